@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s (path segments = paths x bounces per second) on BASELINE.json configs[1]:
+the README Cornell box (frozen C1/C2 scene) at 1920x1080, 8 bounces, 1024 spp.
+
+One step = one full progressive render of that frame: reset, 1024 samples through the trace megakernel,
+and (N > 1) the RCCL sum-reduce of the per-rank float4 accumulators into rank 0. Frames are split into
+64x64 tiles dealt round-robin to ranks (strong scaling: total work fixed). Inputs are resident on the
+device before timing starts (scene rows uploaded by sail_set_scene; the per-sample camera schedule is
+generated on the host and uploaded inside the step, ~64 KB, as the reference uploads uniforms per frame).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
+(one process per GPU, RCCL). Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sail_amd import capi  # noqa: E402
+
+# BASELINE.json configs[1]
+CONFIG = {"workload": "cornell_box_readme_C2", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024}
+FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
+
+
+def load_scene():
+    """The frozen C1/C2 Cornell box rows (captured from the reference's own serializer) + its camera."""
+    path = os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "tests", "golden", "fixtures.json")
+        with open(path) as f:
+            sc = json.load(f)["scenes"]["C1"]
+    else:
+        with open(path) as f:
+            sc = json.load(f)["C1"]
+    return sc
+
+
+def cpu_baseline(sc, masks, mvp, W, H, B):
+    """The CPU oracle (single-threaded C++ restatement of the shader) on a bounded centre crop."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle  # test infrastructure: CPU reference, used here only as the timed baseline
+    cw, ch, spp = 192, 108, 12
+    x0, y0 = (W - cw) // 2, (H - ch) // 2
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    oracle.reset_counters()
+    acc = np.zeros((H, W, 4), np.float32)
+    t0 = time.perf_counter()
+    oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, cw, ch), accum=acc)
+    dt = time.perf_counter() - t0
+    segs = cw * ch * spp * B
+    return {"value": segs / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/sail_oracle.cpp single thread, {cw}x{ch} centre crop of the C2 frame, {spp} spp x {B} "
+                      f"bounces = {segs} nominal segments in {dt:.2f} s"}
+
+
+def ops_per_segment(sc, masks, mvp, W, H, B):
+    """Algorithmic f32 ops per segment from the op-counting oracle build (SURVEY §8(d) op model)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    inv, seeds = capi.schedule(mvp, W, H, 0, 2)
+    oracle.reset_counters(count=True)
+    acc = np.zeros((H, W, 4), np.float32)
+    cw, ch = 64, 36
+    oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=((W - cw) // 2, (H - ch) // 2, cw, ch),
+                  accum=acc, count=True)
+    segs, ops = oracle.counters(count=True)
+    return ops / max(segs, 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=CONFIG["spp"])
+    ap.add_argument("--launch-spp", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+
+    W, H, B, spp = CONFIG["width"], CONFIG["height"], CONFIG["bounces"], args.spp
+    sc = load_scene()
+    masks = capi.plugin_masks(sc["plugins"])
+    # makePerspective(55, W/H, 1, 100) (camera.js:16) with the frozen README camera
+    mvp = capi.camera(sc["eye"], [2.78, 2.73, 2.79], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+
+    ctx = capi.Context(W, H, device=local_rank)
+    ctx.set_scene_dict(sc)
+    ctx.set_launch_samples(args.launch_spp)
+    if world > 1:
+        ctx.set_partition(rank, world, capi.PART_TILES)
+        uid = [capi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], world, rank)
+
+    def step():
+        ctx.reset()
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        if world > 1:
+            ctx.reduce(0)
+
+    def barrier_sync():
+        ctx.sync()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    kernel_ms = 0.0
+    launches = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        ctx.sync()
+        st = ctx.stats()
+        kernel_ms += st.kernel_ms
+        launches += st.launches
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_segments = W * H * spp * B * args.steps  # nominal; closed scene: every path runs all bounces
+    value = total_segments / elapsed / 1e6
+    if rank == 0:
+        avg_launch_s = (kernel_ms / max(launches, 1)) / 1e3
+        # this rank's pixels per launch (rank 0 at N = 1: the full frame)
+        tiles_px = W * H if world == 1 else None
+        if tiles_px is None:
+            tx, ty = (W + 63) // 64, (H + 63) // 64
+            tiles_px = 0
+            for t in range(0, tx * ty, world):
+                tiles_px += min(64, W - (t % tx) * 64) * min(64, H - (t // tx) * 64)
+        segs_per_launch = tiles_px * args.launch_spp * B
+        ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
+        achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
+        hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
+        rec = {
+            "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: frozen README Cornell box rows (reference serializer), deterministic sample schedule",
+            "config": {"workload": CONFIG["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
+                       "launch_spp": args.launch_spp, "partition": f"tiles64x{world}", "segments_per_step": W * H * spp * B},
+            "roofline": {
+                "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "ops_per_segment": round(ops_seg, 2), "kernel": "sail_trace_kernel",
+                "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            rec["cpu_baseline"] = cpu_baseline(sc, masks, mvp, W, H, B)
+        print(json.dumps(rec), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

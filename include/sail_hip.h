@@ -1,0 +1,133 @@
+/* sail_hip.h — C ABI of libsail_hip.so, the MI355X drop-in for Sail's per-frame GPU work.
+ *
+ * Sail drives its hot path through WebGL: Renderer.update(scene) -> Tracer.update uploads the scene
+ * rows as R32F textures and links a generated trace program (src/core/tracer.js:42-90,
+ * src/core/shader.js:58-76); Renderer.render(scene) -> Tracer.render sets the per-frame uniforms and
+ * calls gl.drawArrays (src/core/tracer.js:92-101, src/core/webgl.js:51-93), then RenderShader.render
+ * runs the display filter (src/core/renderer.js:54-72). Each entry point below names the reference
+ * interface it replaces. Plain C types only; the caller owns every host pointer (valid for the call);
+ * the library owns all device memory; no global state; a context is used from one thread.
+ * Every function returns SAIL_OK (0) or a negative SAIL_E_* code; sail_last_error() gives text.
+ * The JS host binds these through the N-API addon in sail_amd/js/native.
+ */
+#ifndef SAIL_HIP_H
+#define SAIL_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAIL_ABI_VERSION 1
+
+enum sail_status {
+  SAIL_OK = 0,
+  SAIL_E_INVALID = -1,   /* bad argument / shape mismatch */
+  SAIL_E_HIP = -2,       /* HIP runtime error */
+  SAIL_E_OOM = -3,       /* device allocation failed */
+  SAIL_E_STATE = -4,     /* call out of order (e.g. render before set_scene) */
+  SAIL_E_RCCL = -5,      /* collective failed or RCCL unavailable */
+  SAIL_E_NODEVICE = -6   /* no HIP device */
+};
+
+/* sail_create flags */
+enum sail_flags {
+  SAIL_FLAG_AOV = 1u << 0,          /* keep the normal/position outputs (fstrace.glsl:15-16) */
+  SAIL_FLAG_SEGMENT_COUNT = 1u << 1 /* exact in-kernel segment counter (sail_stats.segments) */
+};
+/* accumulation modes (sail_set_accum_mode) */
+enum sail_accum_mode {
+  SAIL_ACCUM_SUM = 0,    /* float4 sum + count; mean = sum / count (default, order-independent) */
+  SAIL_ACCUM_MIX = 1,    /* the reference's running mean mix(e, prev, k/(k+1)) (fstrace.glsl:14) */
+  SAIL_ACCUM_COMPAT8 = 2 /* MIX with the per-frame UNORM8 store of a WebGL2 RGB8 frame texture */
+};
+/* multi-GPU partition of one frame (sail_set_partition) */
+enum sail_partition { SAIL_PART_TILES = 0, SAIL_PART_SAMPLES = 1 };
+/* display filters (Scene.filter, src/shader/filter/shader.filter.js:18-30) */
+enum sail_filter_kind { SAIL_FILTER_COLOR = 0, SAIL_FILTER_GAMMA = 1, SAIL_FILTER_TONEMAPPING = 2, SAIL_FILTER_WINDOW = 3 };
+
+/* compiled plugin set (Scene.tracerConfig(), src/scene/scene.js:70-112), as bit masks over category ids:
+ * shape bit = shape id (define.glsl:18-26), material bit = material id (:32-35), texture bit = texture id
+ * (:38-44; UniformColor is always available), light bit = light id (:28-30). */
+typedef struct sail_plugins {
+  uint32_t shape_mask, material_mask, texture_mask, light_mask;
+} sail_plugins;
+
+typedef struct sail_stats {
+  uint64_t samples;          /* samples accumulated since the last reset (this rank) */
+  uint64_t segments;         /* exact segments traced (needs SAIL_FLAG_SEGMENT_COUNT) */
+  uint64_t nominal_segments; /* pixels * samples * max_bounces of the launches since reset */
+  double kernel_ms;          /* sum of trace-kernel durations (HIP events) since reset */
+  double last_launch_ms;     /* duration of the most recent trace launch */
+  uint32_t launches;         /* trace launches since reset */
+} sail_stats;
+
+typedef struct sail_ctx sail_ctx;
+
+/* new Sail.Renderer(canvas) (src/core/renderer.js:9-39): one device, a W x H float accumulator.
+ * device < 0 uses the current device. */
+int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flags);
+void sail_destroy(sail_ctx* ctx);
+const char* sail_last_error(const sail_ctx* ctx); /* ctx may be NULL: last creation error */
+int sail_device_count(int* count);
+
+/* Tracer.update(scene) (src/core/tracer.js:42-90): the objects / texParams / lights rows exactly as
+ * gen() serialises them (18 / 16 / 18 floats per row, Appendix A of SURVEY.md). Copied. */
+int sail_set_scene(sail_ctx* ctx, const float* objects, int n, const float* texparams, int tn,
+                   const float* lights, int ln, const sail_plugins* plugins);
+/* Tracer.updateObjects(scene) (src/core/tracer.js:25-40): new object rows, same n; resets accumulation */
+int sail_update_objects(sail_ctx* ctx, const float* objects, int n);
+
+int sail_set_accum_mode(sail_ctx* ctx, int mode);        /* resets accumulation */
+int sail_set_partition(sail_ctx* ctx, int rank, int world, int mode);
+int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch (default 32) */
+
+/* Tracer.render(mvp, eye, k) (src/core/tracer.js:92-101) = one progressive sample with the caller's
+ * jittered inverse matrix (16 f32, column-major as uniformMatrix4fv uploads it, webgl.js:103) and seed. */
+int sail_render(sail_ctx* ctx, const float inv_mvp[16], const float eye[3], float time_seed, int max_bounces);
+/* spp samples in one call: inv_mvp = spp x 16 floats, seeds = spp floats (a deterministic schedule). */
+int sail_render_schedule(sail_ctx* ctx, const float* inv_mvp, const float* seeds, const float eye[3],
+                         int spp, int max_bounces);
+/* Renderer.render with scene.moving: sampleCount = 0 (src/core/renderer.js:57-60) */
+int sail_reset(sail_ctx* ctx);
+int sail_sync(sail_ctx* ctx);
+
+/* mean image (W*H*4 f32, row 0 = bottom, like glReadPixels), optional AOVs (W*H*4 each) */
+int sail_readback(sail_ctx* ctx, float* rgba, float* normal, float* position);
+/* raw accumulator (SUM: rgb sums + count in .w; MIX: running mean) */
+int sail_read_accum(sail_ctx* ctx, float* rgba);
+/* RenderShader.render (src/core/renderer.js:63) -> pixelFilter (src/shader/filter/<kind>.glsl):
+ * out_rgba = W*H*4 f32 (may be NULL), out_rgba8 = W*H*4 UNORM8 canvas pixels (may be NULL).
+ * weights16 = the 16-entry window table (window filters), radius (rx, ry) in pixels, gamma_c for GAMMA. */
+int sail_filter(sail_ctx* ctx, int kind, const float* weights16, float rx, float ry, float gamma_c,
+                float* out_rgba, uint8_t* out_rgba8);
+int sail_get_stats(sail_ctx* ctx, sail_stats* out);
+
+/* ---- host math of the reference, so every host language gets identical uniforms ---- */
+/* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):
+ * P*MV (scene.mat, src/scene/scene.js:40-42) as 16 doubles, row-major */
+int sail_camera(const double eye[3], const double center[3], const double up[3], double fovy, double aspect,
+                double znear, double zfar, double mvp_rowmajor[16]);
+/* inverse(Translation(jx/W, jy/H, 0) * mvp) flattened column-major in f32 (tracer.js:94-96, matrix.js:501-527) */
+int sail_jitter_inverse(const double mvp_rowmajor[16], double jx, double jy, int width, int height, float inv_colmajor[16]);
+/* The frozen deterministic schedule: sample k uses time_seed = 0.001*round(1000*(k+1)/60)
+ * and jitter from xorshift32(0x5A11 + k). Fills spp x 16 matrices and spp seeds for k = k0 .. k0+spp-1. */
+int sail_schedule(const double mvp_rowmajor[16], int width, int height, int k0, int spp, float* inv_colmajor, float* seeds);
+
+/* ---- multi-GPU (one process per GPU): image tiles / sample split + RCCL sum-reduce of the accumulators ---- */
+int sail_comm_unique_id(char id[128]);
+int sail_comm_init(sail_ctx* ctx, const char id[128], int nranks, int rank);
+int sail_reduce(sail_ctx* ctx, int root);                /* in-place sum of the float4 accumulators into root */
+int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes); /* for an external collective */
+
+/* ---- diagnostics ---- */
+/* evaluate the build's f32 math spec on the device (fn: 0 sin 1 cos 2 tan 3 atan2(y,x) 4 acos 5 pow(x,y)
+ * 6 atan 7 sqrt 8 x/y); for the CPU/GPU bit-parity test */
+int sail_math_probe(int fn, const float* x, const float* y, float* out, int count);
+int sail_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAIL_HIP_H */

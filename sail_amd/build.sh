@@ -1,0 +1,14 @@
+#!/bin/sh
+# Builds libsail_hip.so for gfx950 in-tree (sail_amd/lib/). Contraction is off everywhere: the
+# kernels follow the reference's f32 expression order and the bit-defined math spec (sail_math.h).
+set -e
+cd "$(dirname "$0")"
+mkdir -p lib build
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+ARCH=${SAIL_ARCH:-gfx950}
+COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function"
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_trace.hip -o build/sail_trace.o ${SAIL_EXTRA:-}
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_capi.cpp -o build/sail_capi.o
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_hostmath.cpp -o build/sail_hostmath.o
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o build/sail_capi.o build/sail_hostmath.o \
+  -o lib/libsail_hip.so -ldl

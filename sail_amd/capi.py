@@ -1,0 +1,291 @@
+"""ctypes binding of libsail_hip.so (include/sail_hip.h) for the Python side (tests, bench).
+
+The product host API is the JavaScript one in sail_amd/js (Sail.Renderer / Scene / Camera over the
+N-API addon); this module is the same C ABI seen from Python. It never falls back to anything: if
+the HIP library is missing or a call fails, it raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsail_hip.so")
+
+SAIL_OK = 0
+FLAG_AOV = 1
+FLAG_SEGMENT_COUNT = 2
+ACCUM_SUM, ACCUM_MIX, ACCUM_COMPAT8 = 0, 1, 2
+PART_TILES, PART_SAMPLES = 0, 1
+FILTER_COLOR, FILTER_GAMMA, FILTER_TONEMAPPING, FILTER_WINDOW = 0, 1, 2, 3
+
+# exported symbols (kept in sync with include/sail_hip.h; tests/test_capi_symbols.py checks both ways)
+EXPORTS = (
+    "sail_create", "sail_destroy", "sail_last_error", "sail_device_count", "sail_set_scene",
+    "sail_update_objects", "sail_set_accum_mode", "sail_set_partition", "sail_set_launch_samples",
+    "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
+    "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
+    "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_math_probe",
+    "sail_abi_version",
+)
+
+
+class SailError(RuntimeError):
+    pass
+
+
+class Plugins(ctypes.Structure):
+    _fields_ = [("shape_mask", ctypes.c_uint32), ("material_mask", ctypes.c_uint32),
+                ("texture_mask", ctypes.c_uint32), ("light_mask", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64),
+                ("nominal_segments", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
+                ("last_launch_ms", ctypes.c_double), ("launches", ctypes.c_uint32)]
+
+
+_SHAPES = {"cube": 1, "sphere": 2, "rectangle": 3, "cone": 4, "cylinder": 5, "disk": 6,
+           "hyperboloid": 7, "paraboloid": 8, "cornellbox": 9}
+_MATERIALS = {"matte": 1, "mirror": 2, "metal": 3, "glass": 4}
+_TEXTURES = {"checkerboard": 5, "checkerboard2": 7, "bilerp": 8, "mixf": 9, "scale": 10, "uvf": 11}
+_LIGHTS = {"area": 0, "point": 1, "spot": 2}
+
+
+def plugin_masks(plugins: dict) -> tuple:
+    """Scene.tracerConfig() plugin-name lists -> category bit masks (src/scene/scene.js:70-112)."""
+    def mask(names, table):
+        m = 0
+        for nm in names:
+            m |= 1 << table[nm]
+        return m
+    return (mask(plugins.get("shape", []), _SHAPES), mask(plugins.get("material", []), _MATERIALS),
+            mask(plugins.get("texture", []), _TEXTURES), mask(plugins.get("light", []), _LIGHTS))
+
+
+_lib = None
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libsail_hip.so (raises if it is absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise SailError(f"HIP library not built: {p} (run python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(p)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    f64p = ctypes.POINTER(ctypes.c_double)
+    vp = ctypes.c_void_p
+    sig = {
+        "sail_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]),
+        "sail_destroy": (None, [vp]),
+        "sail_last_error": (ctypes.c_char_p, [vp]),
+        "sail_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "sail_set_scene": (ctypes.c_int, [vp, f32p, ctypes.c_int, f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.POINTER(Plugins)]),
+        "sail_update_objects": (ctypes.c_int, [vp, f32p, ctypes.c_int]),
+        "sail_set_accum_mode": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sail_set_partition": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+        "sail_set_launch_samples": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sail_render": (ctypes.c_int, [vp, f32p, f32p, ctypes.c_float, ctypes.c_int]),
+        "sail_render_schedule": (ctypes.c_int, [vp, f32p, f32p, f32p, ctypes.c_int, ctypes.c_int]),
+        "sail_reset": (ctypes.c_int, [vp]),
+        "sail_sync": (ctypes.c_int, [vp]),
+        "sail_readback": (ctypes.c_int, [vp, f32p, f32p, f32p]),
+        "sail_read_accum": (ctypes.c_int, [vp, f32p]),
+        "sail_filter": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p, ctypes.POINTER(ctypes.c_uint8)]),
+        "sail_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(Stats)]),
+        "sail_camera": (ctypes.c_int, [f64p, f64p, f64p, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, f64p]),
+        "sail_jitter_inverse": (ctypes.c_int, [f64p, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int, f32p]),
+        "sail_schedule": (ctypes.c_int, [f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p, f32p]),
+        "sail_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+        "sail_comm_init": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
+        "sail_reduce": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sail_accum_device_ptr": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]),
+        "sail_math_probe": (ctypes.c_int, [ctypes.c_int, f32p, f32p, f32p, ctypes.c_int]),
+        "sail_abi_version": (ctypes.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _ptr(a: Optional[np.ndarray], ct=ctypes.c_float):
+    if a is None:
+        return ctypes.cast(None, ctypes.POINTER(ct))
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+# ---- host math (no device needed) ----------------------------------------------------------------------
+def camera(eye, center, up=(0.0, 1.0, 0.0), fovy=55.0, aspect=1.0, znear=1.0, zfar=100.0) -> np.ndarray:
+    lib = load()
+    e, c, u = (np.ascontiguousarray(np.asarray(v, dtype=np.float64)) for v in (eye, center, up))
+    out = np.zeros(16, dtype=np.float64)
+    rc = lib.sail_camera(_ptr(e, ctypes.c_double), _ptr(c, ctypes.c_double), _ptr(u, ctypes.c_double),
+                         fovy, aspect, znear, zfar, _ptr(out, ctypes.c_double))
+    if rc:
+        raise SailError(f"sail_camera: {rc}")
+    return out.reshape(4, 4)
+
+
+def jitter_inverse(mvp: np.ndarray, jx: float, jy: float, width: int, height: int) -> np.ndarray:
+    lib = load()
+    m = np.ascontiguousarray(np.asarray(mvp, dtype=np.float64).reshape(16))
+    out = np.zeros(16, dtype=np.float32)
+    rc = lib.sail_jitter_inverse(_ptr(m, ctypes.c_double), jx, jy, width, height, _ptr(out))
+    if rc:
+        raise SailError(f"sail_jitter_inverse: {rc}")
+    return out
+
+
+def schedule(mvp: np.ndarray, width: int, height: int, k0: int, spp: int):
+    """The frozen sample schedule: (spp x 16 f32 inverse matrices, spp f32 seeds)."""
+    lib = load()
+    m = np.ascontiguousarray(np.asarray(mvp, dtype=np.float64).reshape(16))
+    inv = np.zeros((spp, 16), dtype=np.float32)
+    seeds = np.zeros(spp, dtype=np.float32)
+    rc = lib.sail_schedule(_ptr(m, ctypes.c_double), width, height, k0, spp, _ptr(inv), _ptr(seeds))
+    if rc:
+        raise SailError(f"sail_schedule: {rc}")
+    return inv, seeds
+
+
+def math_probe(fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:
+    lib = load()
+    x = _f32(x)
+    y = _f32(np.zeros_like(x) if y is None else y)
+    out = np.zeros_like(x)
+    rc = lib.sail_math_probe(fn, _ptr(x), _ptr(y), _ptr(out), int(x.size))
+    if rc:
+        raise SailError(f"sail_math_probe: {lib.sail_last_error(None).decode()}")
+    return out
+
+
+def device_count() -> int:
+    lib = load()
+    n = ctypes.c_int(0)
+    lib.sail_device_count(ctypes.byref(n))
+    return n.value
+
+
+def comm_unique_id() -> bytes:
+    lib = load()
+    buf = ctypes.create_string_buffer(128)
+    rc = lib.sail_comm_unique_id(buf)
+    if rc:
+        raise SailError(f"sail_comm_unique_id: {lib.sail_last_error(None).decode()}")
+    return buf.raw
+
+
+class Context:
+    """One device context: the MI355X counterpart of Sail's Renderer/Tracer GPU state."""
+
+    def __init__(self, width: int, height: int, device: int = -1, flags: int = 0):
+        self.lib = load()
+        self.W, self.H = int(width), int(height)
+        h = ctypes.c_void_p()
+        rc = self.lib.sail_create(ctypes.byref(h), self.W, self.H, device, flags)
+        if rc:
+            raise SailError(f"sail_create: {rc}: {self.lib.sail_last_error(None).decode()}")
+        self.h = h
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            raise SailError(f"{what}: {rc}: {self.lib.sail_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.sail_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, objects, n: int, texparams, tn: int, lights, ln: int, masks: Sequence[int]):
+        o, t, l = _f32(objects), _f32(texparams), _f32(lights)
+        pl = Plugins(*[int(m) for m in masks])
+        self._check(self.lib.sail_set_scene(self.h, _ptr(o), n, _ptr(t), tn, _ptr(l), ln, ctypes.byref(pl)),
+                    "sail_set_scene")
+
+    def set_scene_dict(self, sc: dict):
+        self.set_scene(sc["objects"], sc["n"], sc["texparams"], sc["tn"], sc["lights"], sc["ln"],
+                       plugin_masks(sc["plugins"]))
+
+    def set_accum_mode(self, mode: int):
+        self._check(self.lib.sail_set_accum_mode(self.h, mode), "sail_set_accum_mode")
+
+    def set_partition(self, rank: int, world: int, mode: int = PART_TILES):
+        self._check(self.lib.sail_set_partition(self.h, rank, world, mode), "sail_set_partition")
+
+    def set_launch_samples(self, spp: int):
+        self._check(self.lib.sail_set_launch_samples(self.h, spp), "sail_set_launch_samples")
+
+    def render_schedule(self, inv: np.ndarray, seeds: np.ndarray, eye, max_bounces: int):
+        inv, seeds, e = _f32(inv), _f32(seeds), _f32(eye)
+        self._check(self.lib.sail_render_schedule(self.h, _ptr(inv), _ptr(seeds), _ptr(e), int(seeds.size), max_bounces),
+                    "sail_render_schedule")
+
+    def render(self, inv: np.ndarray, eye, seed: float, max_bounces: int):
+        inv, e = _f32(inv), _f32(eye)
+        self._check(self.lib.sail_render(self.h, _ptr(inv), _ptr(e), float(seed), max_bounces), "sail_render")
+
+    def reset(self):
+        self._check(self.lib.sail_reset(self.h), "sail_reset")
+
+    def sync(self):
+        self._check(self.lib.sail_sync(self.h), "sail_sync")
+
+    def readback(self, aov: bool = False):
+        rgba = np.zeros((self.H, self.W, 4), dtype=np.float32)
+        n = p = None
+        if aov:
+            n = np.zeros_like(rgba)
+            p = np.zeros_like(rgba)
+        self._check(self.lib.sail_readback(self.h, _ptr(rgba), _ptr(n), _ptr(p)), "sail_readback")
+        return (rgba, n, p) if aov else rgba
+
+    def read_accum(self) -> np.ndarray:
+        rgba = np.zeros((self.H, self.W, 4), dtype=np.float32)
+        self._check(self.lib.sail_read_accum(self.h, _ptr(rgba)), "sail_read_accum")
+        return rgba
+
+    def filter(self, kind: int, weights16=None, rx: float = 0.0, ry: float = 0.0, gamma_c: float = 2.2,
+               want_u8: bool = False):
+        out = np.zeros((self.H, self.W, 4), dtype=np.float32)
+        out8 = np.zeros((self.H, self.W, 4), dtype=np.uint8) if want_u8 else None
+        w = _f32(weights16) if weights16 is not None else None
+        self._check(self.lib.sail_filter(self.h, kind, _ptr(w), rx, ry, gamma_c, _ptr(out),
+                                         _ptr(out8, ctypes.c_uint8)), "sail_filter")
+        return (out, out8) if want_u8 else out
+
+    def stats(self) -> Stats:
+        s = Stats()
+        self._check(self.lib.sail_get_stats(self.h, ctypes.byref(s)), "sail_get_stats")
+        return s
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        self._check(self.lib.sail_comm_init(self.h, uid, nranks, rank), "sail_comm_init")
+
+    def reduce(self, root: int = 0):
+        self._check(self.lib.sail_reduce(self.h, root), "sail_reduce")
+
+    def accum_device_ptr(self):
+        p = ctypes.c_void_p()
+        b = ctypes.c_size_t()
+        self._check(self.lib.sail_accum_device_ptr(self.h, ctypes.byref(p), ctypes.byref(b)), "sail_accum_device_ptr")
+        return p.value, b.value

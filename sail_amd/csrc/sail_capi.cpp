@@ -1,0 +1,650 @@
+// sail_capi.cpp — libsail_hip.so: context, scene decode, launches, readback, filter, RCCL reduce.
+// The C ABI is declared (with the reference interface each entry replaces) in include/sail_hip.h.
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <string>
+#include <vector>
+#include "../../include/sail_hip.h"
+#include "sail_device.h"
+
+// launch wrappers defined next to the kernels (sail_trace.hip)
+hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
+hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
+hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+// ---- RCCL, bound at run time (the process may already hold torch's copy under the same soname) ----
+typedef struct { char internal[128]; } nccl_uid_t;
+typedef void* nccl_comm_t;
+struct Rccl {
+  bool tried = false, ok = false;
+  int (*getUniqueId)(nccl_uid_t*) = nullptr;
+  int (*commInitRank)(nccl_comm_t*, int, nccl_uid_t, int) = nullptr;
+  int (*reduce)(const void*, void*, size_t, int, int, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*commDestroy)(nccl_comm_t) = nullptr;
+  const char* (*errStr)(int) = nullptr;
+  bool load() {
+    if (tried) return ok;
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return false;
+    getUniqueId = (int (*)(nccl_uid_t*))dlsym(h, "ncclGetUniqueId");
+    commInitRank = (int (*)(nccl_comm_t*, int, nccl_uid_t, int))dlsym(h, "ncclCommInitRank");
+    reduce = (int (*)(const void*, void*, size_t, int, int, int, nccl_comm_t, hipStream_t))dlsym(h, "ncclReduce");
+    commDestroy = (int (*)(nccl_comm_t))dlsym(h, "ncclCommDestroy");
+    errStr = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+    ok = getUniqueId && commInitRank && reduce && commDestroy;
+    return ok;
+  }
+};
+Rccl g_rccl;
+constexpr int kNcclFloat32 = 7, kNcclSum = 0;
+
+// ---- the reference's texture addressing (texhelper.glsl, NEAREST + CLAMP_TO_EDGE) ----------------------
+int texel(float c, int size) {
+  if (c != c) return 0;  // NaN row coordinate (n = 1 / ln = 1: 0/0) addresses texel 0
+  const float s = floorf(c * (float)size);
+  if (!(s >= 0.0f)) return 0;
+  if (s >= (float)(size - 1)) return size - 1;
+  return (int)s;
+}
+int to_int(float x) {
+  if (x != x) return 0;
+  if (x >= 2147483647.0f) return 2147483647;
+  if (x <= -2147483648.0f) return (-2147483647 - 1);
+  return (int)x;
+}
+struct TexView {
+  const float* d; int w, h;
+  float at(float cx, float cy) const {
+    if (h <= 0) return 0.0f;
+    return d[texel(cy, h) * w + texel(cx, w)];
+  }
+  float readFloat(float x, float y, float width) const { return at(x / width, y); }
+  void readVec3(float x, float y, float width, float* out) const {
+    float px = x / width;
+    out[0] = at(px, y); px += 1.0f / width;
+    out[1] = at(px, y); px += 1.0f / width;
+    out[2] = at(px, y);
+  }
+};
+
+}  // namespace
+
+struct sail_ctx {
+  int device = 0, W = 0, H = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  float4* accum = nullptr;
+  float4* aovN = nullptr;
+  float4* aovP = nullptr;
+  unsigned long long* segCounter = nullptr;
+  SailPrim* prims = nullptr;
+  float* tp = nullptr;
+  float* lt = nullptr;
+  int32_t* lightObjRow = nullptr;
+  SailSample* samples = nullptr;
+  int samplesCap = 0;
+  std::vector<SailSample> hostSamples;
+  std::vector<float> objectsRows;
+  int n = 0, tn = 0, ln = 0;
+  sail_plugins plugins{};
+  bool haveScene = false;
+  int shadowAnyHit = 0;
+  int accumMode = SAIL_ACCUM_SUM;
+  int rank = 0, world = 1, partMode = SAIL_PART_TILES;
+  int launchSpp = 32;
+  uint64_t k = 0;  // global sample index of the next sample (the reference's sampleCount)
+  uint64_t samplesThisRank = 0;
+  uint64_t nominalSegments = 0;
+  std::vector<hipEvent_t> evPool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double kernelMs = 0.0, lastLaunchMs = 0.0;
+  uint32_t launches = 0;
+  nccl_comm_t comm = nullptr;
+  int commRanks = 0, commRank = 0;
+  float eyeCache[3] = {0.0f, 0.0f, 0.0f};
+  std::string err;
+};
+
+namespace {
+
+int fail(sail_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf; else g_create_error = buf;
+  return code;
+}
+#define HIPCHK(ctx, call)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess) return fail((ctx), SAIL_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
+  const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
+  *tilesX = tx; *tilesY = ty;
+  if (c->partMode == SAIL_PART_SAMPLES) return tx * ty;
+  const int total = tx * ty;
+  return c->rank < total ? (total - c->rank + c->world - 1) / c->world : 0;
+}
+long long ownedPixels(const sail_ctx* c) {
+  int tx, ty;
+  const int owned = ownedTiles(c, &tx, &ty);
+  long long px = 0;
+  const int w = (c->partMode == SAIL_PART_SAMPLES) ? 1 : c->world, r = (c->partMode == SAIL_PART_SAMPLES) ? 0 : c->rank;
+  for (int j = 0; j < owned; j++) {
+    const int t = r + j * w;
+    const int x0 = (t % tx) * 64, y0 = (t / tx) * 64;
+    const int cw = (c->W - x0) < 64 ? (c->W - x0) : 64, ch = (c->H - y0) < 64 ? (c->H - y0) : 64;
+    px += (long long)cw * ch;
+  }
+  return px;
+}
+
+int collectEvents(sail_ctx* c) {
+  for (auto& pr : c->pending) {
+    HIPCHK(c, hipEventSynchronize(pr.second));
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    c->kernelMs += ms;
+    c->lastLaunchMs = ms;
+    c->evPool.push_back(pr.first);
+    c->evPool.push_back(pr.second);
+  }
+  c->pending.clear();
+  return SAIL_OK;
+}
+int getEvent(sail_ctx* c, hipEvent_t* ev) {
+  if (!c->evPool.empty()) { *ev = c->evPool.back(); c->evPool.pop_back(); return SAIL_OK; }
+  HIPCHK(c, hipEventCreate(ev));
+  return SAIL_OK;
+}
+
+// corner directions of vstrace.glsl:4-6 for one jittered inverse matrix (column-major, f32)
+void cornerDirs(const float* M, const float* eye, float out[4][3]) {
+  static const float cx[4] = {-1.0f, -1.0f, 1.0f, 1.0f}, cy[4] = {-1.0f, 1.0f, -1.0f, 1.0f};
+  for (int c = 0; c < 4; c++) {
+    float q[4];
+    for (int r = 0; r < 4; r++) q[r] = M[0 * 4 + r] * cx[c] + M[1 * 4 + r] * cy[c] + M[2 * 4 + r] * 0.0f + M[3 * 4 + r] * 1.0f;
+    const float w[3] = {q[0] / q[3] - eye[0], q[1] / q[3] - eye[1], q[2] / q[3] - eye[2]};
+    const float len = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    out[c][0] = w[0] / len; out[c][1] = w[1] / len; out[c][2] = w[2] / len;
+  }
+}
+
+int resetAccum(sail_ctx* c) {
+  const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  HIPCHK(c, hipMemsetAsync(c->accum, 0, bytes, c->stream));
+  if (c->aovN) HIPCHK(c, hipMemsetAsync(c->aovN, 0, bytes, c->stream));
+  if (c->aovP) HIPCHK(c, hipMemsetAsync(c->aovP, 0, bytes, c->stream));
+  if (c->segCounter) HIPCHK(c, hipMemsetAsync(c->segCounter, 0, sizeof(unsigned long long), c->stream));
+  int rc = collectEvents(c);
+  if (rc) return rc;
+  c->k = 0;
+  c->samplesThisRank = 0;
+  c->nominalSegments = 0;
+  c->kernelMs = 0.0;
+  c->lastLaunchMs = 0.0;
+  c->launches = 0;
+  return SAIL_OK;
+}
+
+// Decode the objects rows into SailPrim records with the reference's addressing rules
+// (shader.shape.js:34 row = float(i)/float(n-1); parseX readFloat/readVec3 columns; matIndex/texIndex as
+// readFloat(...)/float(tn-1) normalised rows; cornellbox.glsl:17 material from slot 7).
+void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk) {
+  TexView o{objects, 18, n};
+  const float L = 17.0f;
+  out.assign((size_t)n, SailPrim{});
+  *anyHitOk = 1;
+  auto row = [&](float v) { return texel(v / (float)(tn - 1), tn); };
+  for (int i = 0; i < n; i++) {
+    const float rc = (float)i / (float)(n - 1);
+    SailPrim& p = out[i];
+    memset(&p, 0, sizeof p);
+    const int cat = to_int(o.at(0.0f, rc));
+    if (cat < 1 || cat > 9 || !((shapeMask >> cat) & 1u)) { p.type = 0; continue; }
+    p.type = cat;
+    float v3[3];
+    switch (cat) {
+      case SAIL_CUBE: case SAIL_RECTANGLE:
+        o.readVec3(1.0f, rc, L, &p.a[0]); o.readVec3(4.0f, rc, L, &p.a[3]);
+        p.rev = to_int(o.readFloat(7.0f, rc, L)) == 1;
+        p.matRow = row(o.readFloat(8.0f, rc, L)); p.texRow = row(o.readFloat(9.0f, rc, L));
+        o.readVec3(10.0f, rc, L, v3);
+        break;
+      case SAIL_SPHERE:
+        o.readVec3(1.0f, rc, L, &p.a[0]); p.a[3] = o.readFloat(4.0f, rc, L);
+        p.rev = to_int(o.readFloat(5.0f, rc, L)) == 1;
+        p.matRow = row(o.readFloat(6.0f, rc, L)); p.texRow = row(o.readFloat(7.0f, rc, L));
+        o.readVec3(8.0f, rc, L, v3);
+        break;
+      case SAIL_CONE: case SAIL_CYLINDER: case SAIL_DISK:  // p3, (h r) or (r innerR)
+        o.readVec3(1.0f, rc, L, &p.a[0]); p.a[3] = o.readFloat(4.0f, rc, L); p.a[4] = o.readFloat(5.0f, rc, L);
+        p.rev = to_int(o.readFloat(6.0f, rc, L)) == 1;
+        p.matRow = row(o.readFloat(7.0f, rc, L)); p.texRow = row(o.readFloat(8.0f, rc, L));
+        o.readVec3(9.0f, rc, L, v3);
+        break;
+      case SAIL_HYPERBOLOID:
+        o.readVec3(1.0f, rc, L, &p.a[0]); o.readVec3(4.0f, rc, L, &p.a[3]); o.readVec3(7.0f, rc, L, &p.a[6]);
+        p.a[9] = o.readFloat(10.0f, rc, L); p.a[10] = o.readFloat(11.0f, rc, L);
+        p.rev = to_int(o.readFloat(12.0f, rc, L)) == 1;
+        p.matRow = row(o.readFloat(13.0f, rc, L)); p.texRow = row(o.readFloat(14.0f, rc, L));
+        o.readVec3(15.0f, rc, L, v3);
+        break;
+      case SAIL_PARABOLOID:
+        o.readVec3(1.0f, rc, L, &p.a[0]);
+        p.a[3] = o.readFloat(4.0f, rc, L); p.a[4] = o.readFloat(5.0f, rc, L); p.a[5] = o.readFloat(6.0f, rc, L);
+        p.rev = to_int(o.readFloat(7.0f, rc, L)) == 1;
+        p.matRow = row(o.readFloat(8.0f, rc, L)); p.texRow = row(o.readFloat(9.0f, rc, L));
+        o.readVec3(10.0f, rc, L, v3);
+        break;
+      case SAIL_CORNELLBOX:
+        o.readVec3(1.0f, rc, L, &p.a[0]); o.readVec3(4.0f, rc, L, &p.a[3]);
+        p.rev = 0;
+        p.matRow = row(o.readFloat(7.0f, rc, L));  // slot 7 = reverseNormal (cornellbox.glsl:17)
+        p.texRow = 0;
+        v3[0] = v3[1] = v3[2] = 0.0f;
+        break;
+      default: break;
+    }
+    p.em[0] = v3[0]; p.em[1] = v3[1]; p.em[2] = v3[2];
+    // only slabs return t > EPSILON strictly; anything else may tie or undercut EPSILON, so shadow
+    // rays must then find the true closest distance (shader.light.js:24-31)
+    if (cat != SAIL_CUBE && cat != SAIL_CORNELLBOX) *anyHitOk = 0;
+  }
+}
+
+int ensureSamples(sail_ctx* c, int count) {
+  if (count <= c->samplesCap) return SAIL_OK;
+  if (c->samples) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->samples)); c->samples = nullptr; }
+  int cap = 64;
+  while (cap < count) cap *= 2;
+  if (hipMalloc(&c->samples, sizeof(SailSample) * cap) != hipSuccess) return fail(c, SAIL_E_OOM, "sample buffer");
+  c->samplesCap = cap;
+  return SAIL_OK;
+}
+
+int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
+  int tx, ty;
+  const int owned = ownedTiles(c, &tx, &ty);
+  if (count <= 0 || owned <= 0) return SAIL_OK;
+  int rc = ensureSamples(c, count);
+  if (rc) return rc;
+  // the upload is ordered with the launch on the context stream
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->samples, hs, sizeof(SailSample) * count, hipMemcpyHostToDevice, c->stream));
+  const long long px = ownedPixels(c);
+  for (int s0 = 0; s0 < count; s0 += c->launchSpp) {
+    const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
+    SailTraceArgs A;
+    memset(&A, 0, sizeof A);
+    A.prims = c->prims; A.texparams = c->tp; A.lights = c->lt; A.lightObjRow = c->lightObjRow;
+    A.samples = c->samples + s0;
+    A.accum = c->accum; A.aovN = c->aovN; A.aovP = c->aovP; A.segCounter = c->segCounter;
+    A.W = c->W; A.H = c->H; A.n = c->n; A.tn = c->tn; A.ln = c->ln;
+    A.matMask = c->plugins.material_mask; A.texMask = c->plugins.texture_mask; A.lightMask = c->plugins.light_mask;
+    A.maxBounces = maxBounces; A.spp = nspp; A.accumMode = c->accumMode;
+    A.tilesX = tx; A.tilesY = ty;
+    A.world = (c->partMode == SAIL_PART_SAMPLES) ? 1 : c->world;
+    A.rank = (c->partMode == SAIL_PART_SAMPLES) ? 0 : c->rank;
+    A.ownedTiles = owned;
+    A.shadowAnyHit = c->shadowAnyHit;
+    memcpy(A.eye, c->eyeCache, sizeof A.eye);
+    hipEvent_t e0, e1;
+    if ((rc = getEvent(c, &e0)) || (rc = getEvent(c, &e1))) return rc;
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    HIPCHK(c, sail_launch_trace(A, owned * 16, c->stream));
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    c->pending.emplace_back(e0, e1);
+    c->launches++;
+    c->nominalSegments += (uint64_t)px * (uint64_t)nspp * (uint64_t)maxBounces;
+  }
+  return SAIL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sail_abi_version(void) { return SAIL_ABI_VERSION; }
+
+int sail_device_count(int* count) {
+  if (!count) return SAIL_E_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return SAIL_OK;
+}
+
+const char* sail_last_error(const sail_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flags) {
+  if (!out || width <= 0 || height <= 0 || width > 32768 || height > 32768)
+    return fail(nullptr, SAIL_E_INVALID, "sail_create: bad arguments %dx%d", width, height);
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(nullptr, SAIL_E_NODEVICE, "no HIP device");
+  if (device < 0) { if (hipGetDevice(&device) != hipSuccess) device = 0; }
+  if (device >= ndev) return fail(nullptr, SAIL_E_INVALID, "device %d out of range (%d devices)", device, ndev);
+  sail_ctx* c = new sail_ctx();
+  c->device = device; c->W = width; c->H = height; c->flags = flags;
+  auto bail = [&](int code, const char* what) {
+    g_create_error = std::string("sail_create: ") + what;
+    sail_destroy(c);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(SAIL_E_HIP, "hipSetDevice");
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(SAIL_E_HIP, "stream");
+  const size_t bytes = (size_t)width * height * sizeof(float4);
+  if (hipMalloc(&c->accum, bytes) != hipSuccess) return bail(SAIL_E_OOM, "accumulator");
+  if (flags & SAIL_FLAG_AOV) {
+    if (hipMalloc(&c->aovN, bytes) != hipSuccess || hipMalloc(&c->aovP, bytes) != hipSuccess) return bail(SAIL_E_OOM, "aov");
+  }
+  if (flags & SAIL_FLAG_SEGMENT_COUNT) {
+    if (hipMalloc(&c->segCounter, sizeof(unsigned long long)) != hipSuccess) return bail(SAIL_E_OOM, "counter");
+  }
+  if (resetAccum(c) != SAIL_OK) return bail(SAIL_E_HIP, c->err.c_str());
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(SAIL_E_HIP, "sync");
+  *out = c;
+  return SAIL_OK;
+}
+
+void sail_destroy(sail_ctx* c) {
+  if (!c) return;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
+  for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto e : c->evPool) (void)hipEventDestroy(e);
+  void* bufs[] = {c->accum, c->aovN, c->aovP, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
+  for (void* b : bufs) if (b) (void)hipFree(b);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texparams, int tn, const float* lights,
+                   int ln, const sail_plugins* plugins) {
+  if (!c) return SAIL_E_INVALID;
+  if (n < 0 || tn < 0 || ln < 0 || (n > 0 && !objects) || (tn > 0 && !texparams) || (ln > 0 && !lights) || !plugins)
+    return fail(c, SAIL_E_INVALID, "sail_set_scene: bad arguments (n=%d tn=%d ln=%d)", n, tn, ln);
+  if (n > 0 && tn < 1) return fail(c, SAIL_E_INVALID, "sail_set_scene: objects need texParams rows");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->plugins = *plugins;
+  std::vector<SailPrim> prims;
+  decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit);
+  // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
+  std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
+  TexView lv{lights, 18, ln};
+  for (int r = 0; r < ln; r++) {
+    const float rc = (ln == 1) ? NAN : (float)r / (float)(ln - 1);
+    const int gi = to_int(lv.readFloat(1.0f, rc, 17.0f));
+    lrow[r] = (n > 0) ? texel((float)gi / (float)(n - 1), n) : 0;
+  }
+  void* old[] = {c->prims, c->tp, c->lt, c->lightObjRow};
+  for (void* b : old) if (b) HIPCHK(c, hipFree(b));
+  c->prims = nullptr; c->tp = nullptr; c->lt = nullptr; c->lightObjRow = nullptr;
+  const size_t pb = sizeof(SailPrim) * (size_t)(n > 0 ? n : 1), tb = sizeof(float) * 16 * (size_t)(tn > 0 ? tn : 1),
+               lb = sizeof(float) * 18 * (size_t)(ln > 0 ? ln : 1), rb = sizeof(int32_t) * lrow.size();
+  if (hipMalloc(&c->prims, pb) != hipSuccess || hipMalloc(&c->tp, tb) != hipSuccess || hipMalloc(&c->lt, lb) != hipSuccess ||
+      hipMalloc(&c->lightObjRow, rb) != hipSuccess)
+    return fail(c, SAIL_E_OOM, "scene buffers");
+  HIPCHK(c, hipMemsetAsync(c->tp, 0, tb, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->lt, 0, lb, c->stream));
+  if (n > 0) HIPCHK(c, hipMemcpyAsync(c->prims, prims.data(), sizeof(SailPrim) * n, hipMemcpyHostToDevice, c->stream));
+  if (tn > 0) HIPCHK(c, hipMemcpyAsync(c->tp, texparams, sizeof(float) * 16 * tn, hipMemcpyHostToDevice, c->stream));
+  if (ln > 0) HIPCHK(c, hipMemcpyAsync(c->lt, lights, sizeof(float) * 18 * ln, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->lightObjRow, lrow.data(), rb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->objectsRows.assign(objects, objects + (size_t)n * 18);
+  c->n = n; c->tn = tn; c->ln = ln;
+  c->haveScene = true;
+  return resetAccum(c);
+}
+
+int sail_update_objects(sail_ctx* c, const float* objects, int n) {
+  if (!c || !c->haveScene) return c ? fail(c, SAIL_E_STATE, "sail_update_objects before sail_set_scene") : SAIL_E_INVALID;
+  if (n != c->n || !objects) return fail(c, SAIL_E_INVALID, "sail_update_objects: n must stay %d", c->n);
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<SailPrim> prims;
+  decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (n > 0) HIPCHK(c, hipMemcpyAsync(c->prims, prims.data(), sizeof(SailPrim) * n, hipMemcpyHostToDevice, c->stream));
+  c->objectsRows.assign(objects, objects + (size_t)n * 18);
+  return resetAccum(c);
+}
+
+int sail_set_accum_mode(sail_ctx* c, int mode) {
+  if (!c) return SAIL_E_INVALID;
+  if (mode < SAIL_ACCUM_SUM || mode > SAIL_ACCUM_COMPAT8) return fail(c, SAIL_E_INVALID, "accum mode %d", mode);
+  if (mode != SAIL_ACCUM_SUM && c->partMode == SAIL_PART_SAMPLES && c->world > 1)
+    return fail(c, SAIL_E_INVALID, "running-mean accumulation cannot be split by samples");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->accumMode = mode;
+  return resetAccum(c);
+}
+
+int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
+  if (!c) return SAIL_E_INVALID;
+  if (world < 1 || rank < 0 || rank >= world || (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
+    return fail(c, SAIL_E_INVALID, "partition rank=%d world=%d mode=%d", rank, world, mode);
+  if (mode == SAIL_PART_SAMPLES && world > 1 && c->accumMode != SAIL_ACCUM_SUM)
+    return fail(c, SAIL_E_INVALID, "sample partition needs SAIL_ACCUM_SUM");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->rank = rank; c->world = world; c->partMode = mode;
+  return resetAccum(c);
+}
+
+int sail_set_launch_samples(sail_ctx* c, int spp) {
+  if (!c) return SAIL_E_INVALID;
+  if (spp < 1 || spp > 1 << 20) return fail(c, SAIL_E_INVALID, "launch samples %d", spp);
+  c->launchSpp = spp;
+  return SAIL_OK;
+}
+
+int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, const float eye[3], int spp, int maxBounces) {
+  if (!c) return SAIL_E_INVALID;
+  if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_render before sail_set_scene");
+  if (spp < 0 || (spp > 0 && (!inv || !seeds)) || !eye || maxBounces < 0 || maxBounces > 1024)
+    return fail(c, SAIL_E_INVALID, "sail_render_schedule: bad arguments (spp=%d bounces=%d)", spp, maxBounces);
+  HIPCHK(c, hipSetDevice(c->device));
+  memcpy(c->eyeCache, eye, sizeof(float) * 3);
+  c->hostSamples.clear();
+  for (int s = 0; s < spp; s++) {
+    const uint64_t k = c->k + (uint64_t)s;
+    if (c->partMode == SAIL_PART_SAMPLES && c->world > 1 && (int)(k % (uint64_t)c->world) != c->rank) continue;
+    SailSample S;
+    memset(&S, 0, sizeof S);
+    cornerDirs(inv + 16 * s, eye, S.d);
+    S.seed = seeds[s];
+    S.mixw = (float)((double)k / (double)(k + 1));  // tracer.js:97, f64 then uniform1f
+    c->hostSamples.push_back(S);
+  }
+  const int rc = launchTrace(c, c->hostSamples.data(), (int)c->hostSamples.size(), maxBounces);
+  if (rc) return rc;
+  c->samplesThisRank += c->hostSamples.size();
+  c->k += (uint64_t)spp;
+  return SAIL_OK;
+}
+
+int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed, int maxBounces) {
+  return sail_render_schedule(c, inv, &seed, eye, 1, maxBounces);
+}
+
+int sail_reset(sail_ctx* c) {
+  if (!c) return SAIL_E_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  return resetAccum(c);
+}
+
+int sail_sync(sail_ctx* c) {
+  if (!c) return SAIL_E_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return collectEvents(c);
+}
+
+int sail_read_accum(sail_ctx* c, float* rgba) {
+  if (!c || !rgba) return SAIL_E_INVALID;
+  int rc = sail_sync(c);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy(rgba, c->accum, (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
+  return SAIL_OK;
+}
+
+int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
+  if (!c) return SAIL_E_INVALID;
+  int rc = sail_sync(c);
+  if (rc) return rc;
+  const size_t np = (size_t)c->W * c->H, bytes = np * sizeof(float4);
+  if (rgba) {
+    HIPCHK(c, hipMemcpy(rgba, c->accum, bytes, hipMemcpyDeviceToHost));
+    if (c->accumMode == SAIL_ACCUM_SUM) {
+      for (size_t i = 0; i < np; i++) {
+        const float cnt = rgba[4 * i + 3];
+        if (cnt > 0.0f) { rgba[4 * i] /= cnt; rgba[4 * i + 1] /= cnt; rgba[4 * i + 2] /= cnt; }
+        rgba[4 * i + 3] = 1.0f;
+      }
+    }
+  }
+  if (normal) {
+    if (!c->aovN) return fail(c, SAIL_E_STATE, "AOVs not enabled (SAIL_FLAG_AOV)");
+    HIPCHK(c, hipMemcpy(normal, c->aovN, bytes, hipMemcpyDeviceToHost));
+  }
+  if (position) {
+    if (!c->aovP) return fail(c, SAIL_E_STATE, "AOVs not enabled (SAIL_FLAG_AOV)");
+    HIPCHK(c, hipMemcpy(position, c->aovP, bytes, hipMemcpyDeviceToHost));
+  }
+  return SAIL_OK;
+}
+
+int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float ry, float gammaC, float* out, uint8_t* out8) {
+  if (!c) return SAIL_E_INVALID;
+  if (kind < SAIL_FILTER_COLOR || kind > SAIL_FILTER_WINDOW || (kind == SAIL_FILTER_WINDOW && !weights16))
+    return fail(c, SAIL_E_INVALID, "sail_filter: kind %d", kind);
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = sail_sync(c);
+  if (rc) return rc;
+  const size_t np = (size_t)c->W * c->H;
+  float4* dOut = nullptr;
+  uint8_t* dOut8 = nullptr;
+  if (out && hipMalloc(&dOut, np * sizeof(float4)) != hipSuccess) return fail(c, SAIL_E_OOM, "filter output");
+  if (out8 && hipMalloc(&dOut8, np * 4) != hipSuccess) { if (dOut) (void)hipFree(dOut); return fail(c, SAIL_E_OOM, "filter output"); }
+  SailFilterArgs A;
+  memset(&A, 0, sizeof A);
+  A.accum = c->accum; A.out = dOut; A.out8 = dOut8; A.W = c->W; A.H = c->H; A.kind = kind; A.accumMode = c->accumMode;
+  // a SUM accumulator holds the same count in every pixel of a frame (all pixels get every sample)
+  float cnt = 1.0f;
+  if (c->accumMode == SAIL_ACCUM_SUM) {
+    float4 px0;
+    HIPCHK(c, hipMemcpy(&px0, c->accum, sizeof px0, hipMemcpyDeviceToHost));
+    cnt = px0.w > 0.0f ? px0.w : 1.0f;
+  }
+  A.count = cnt; A.invCount = 1.0f / cnt;
+  if (weights16) memcpy(A.weights, weights16, sizeof A.weights);
+  A.rx = rx; A.ry = ry; A.gammaC = gammaC;
+  hipError_t e = sail_launch_filter(A, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && out) e = hipMemcpy(out, dOut, np * sizeof(float4), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && out8) e = hipMemcpy(out8, dOut8, np * 4, hipMemcpyDeviceToHost);
+  if (dOut) (void)hipFree(dOut);
+  if (dOut8) (void)hipFree(dOut8);
+  if (e != hipSuccess) return fail(c, SAIL_E_HIP, "sail_filter: %s", hipGetErrorString(e));
+  return SAIL_OK;
+}
+
+int sail_get_stats(sail_ctx* c, sail_stats* s) {
+  if (!c || !s) return SAIL_E_INVALID;
+  int rc = sail_sync(c);
+  if (rc) return rc;
+  memset(s, 0, sizeof *s);
+  s->samples = c->samplesThisRank;
+  s->nominal_segments = c->nominalSegments;
+  s->kernel_ms = c->kernelMs;
+  s->last_launch_ms = c->lastLaunchMs;
+  s->launches = c->launches;
+  if (c->segCounter) {
+    unsigned long long v = 0;
+    HIPCHK(c, hipMemcpy(&v, c->segCounter, sizeof v, hipMemcpyDeviceToHost));
+    s->segments = v;
+  }
+  return SAIL_OK;
+}
+
+int sail_accum_device_ptr(sail_ctx* c, void** ptr, size_t* bytes) {
+  if (!c || !ptr || !bytes) return SAIL_E_INVALID;
+  *ptr = c->accum;
+  *bytes = (size_t)c->W * c->H * sizeof(float4);
+  return SAIL_OK;
+}
+
+int sail_comm_unique_id(char id[128]) {
+  if (!id) return SAIL_E_INVALID;
+  if (!g_rccl.load()) return fail(nullptr, SAIL_E_RCCL, "librccl not loadable");
+  nccl_uid_t u;
+  const int r = g_rccl.getUniqueId(&u);
+  if (r) return fail(nullptr, SAIL_E_RCCL, "ncclGetUniqueId: %d", r);
+  memcpy(id, u.internal, 128);
+  return SAIL_OK;
+}
+
+int sail_comm_init(sail_ctx* c, const char id[128], int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return SAIL_E_INVALID;
+  if (!g_rccl.load()) return fail(c, SAIL_E_RCCL, "librccl not loadable");
+  HIPCHK(c, hipSetDevice(c->device));
+  nccl_uid_t u;
+  memcpy(u.internal, id, 128);
+  const int r = g_rccl.commInitRank(&c->comm, nranks, u, rank);
+  if (r) return fail(c, SAIL_E_RCCL, "ncclCommInitRank: %s", g_rccl.errStr ? g_rccl.errStr(r) : "?");
+  c->commRanks = nranks; c->commRank = rank;
+  return SAIL_OK;
+}
+
+int sail_reduce(sail_ctx* c, int root) {
+  if (!c) return SAIL_E_INVALID;
+  if (!c->comm) return fail(c, SAIL_E_STATE, "sail_reduce before sail_comm_init");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t count = (size_t)c->W * c->H * 4;
+  const int r = g_rccl.reduce(c->accum, c->accum, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  if (r) return fail(c, SAIL_E_RCCL, "ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(r) : "?");
+  return SAIL_OK;
+}
+
+int sail_math_probe(int fn, const float* x, const float* y, float* out, int count) {
+  if (!x || !y || !out || count < 0) return SAIL_E_INVALID;
+  if (count == 0) return SAIL_OK;
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t b = sizeof(float) * count;
+  if (hipMalloc(&dx, b) != hipSuccess || hipMalloc(&dy, b) != hipSuccess || hipMalloc(&dout, b) != hipSuccess) {
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    return fail(nullptr, SAIL_E_OOM, "math probe buffers");
+  }
+  hipError_t e = hipMemcpy(dx, x, b, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dy, y, b, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    e = sail_launch_math(fn, dx, dy, dout, count);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out, dout, b, hipMemcpyDeviceToHost);
+  (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dout);
+  if (e != hipSuccess) return fail(nullptr, SAIL_E_HIP, "math probe: %s", hipGetErrorString(e));
+  return SAIL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// sail_device.h — device-side data layout shared by the trace/filter kernels and the host library.
+// All structs are POD, 16-byte aligned, and identical on host and device.
+#pragma once
+#include <stdint.h>
+
+// Shape / material / texture / light category ids (src/shader/const/define.glsl:18-44)
+enum {
+  SAIL_CUBE = 1, SAIL_SPHERE = 2, SAIL_RECTANGLE = 3, SAIL_CONE = 4, SAIL_CYLINDER = 5, SAIL_DISK = 6,
+  SAIL_HYPERBOLOID = 7, SAIL_PARABOLOID = 8, SAIL_CORNELLBOX = 9
+};
+enum { SAIL_AREA = 0, SAIL_POINT = 1, SAIL_SPOT = 2 };
+enum { SAIL_MATTE = 1, SAIL_MIRROR = 2, SAIL_METAL = 3, SAIL_GLASS = 4 };
+enum {
+  SAIL_TEX_UNIFORM = 0, SAIL_TEX_CHECKERBOARD = 5, SAIL_TEX_CHECKERBOARD2 = 7, SAIL_TEX_BILERP = 8,
+  SAIL_TEX_MIXF = 9, SAIL_TEX_SCALE = 10, SAIL_TEX_UVF = 11
+};
+
+// One decoded primitive: the row of the `objects` texture (tracer.js:45-52, webgl.js:137) resolved once on
+// the host with the reference's texture-addressing rules (texhelper.glsl) into integer rows and typed
+// parameters. 128 B, read by the primitive loop with a wave-uniform index (scalar loads).
+struct __attribute__((aligned(16))) SailPrim {
+  int32_t type;     // shape id, 0 when the shape's plugin is not compiled in (never hit)
+  int32_t rev;      // reverseNormal (readBool: int(v) == 1)
+  int32_t matRow;   // texParams row of the material (Cornellbox: slot 7 quirk resolved here)
+  int32_t texRow;   // texParams row of the texture
+  float em[3];      // emission (Cornellbox: forced BLACK, cornellbox.glsl:19)
+  float pad0;
+  float a[24];      // shape parameters in row order (see sail_scene.cpp decode)
+};
+
+// Per-sample uniforms (the reference's per-frame `matrix` + `timeSinceStart` + `textureWeight`,
+// tracer.js:92-101) pre-reduced on the host to the 4 normalised corner directions the vertex
+// shader produces (vstrace.glsl:4-6).
+struct __attribute__((aligned(16))) SailSample {
+  float d[4][3];    // corner directions v0=(-1,-1) v1=(-1,1) v2=(1,-1) v3=(1,1)
+  float seed;       // timeSinceStart
+  float mixw;       // f32(k/(k+1))
+  float pad[2];
+};
+
+struct SailTraceArgs {
+  const SailPrim* prims;
+  const float* texparams;   // tn x 16
+  const float* lights;      // ln x 18
+  const int32_t* lightObjRow;  // per light row: decoded object row of the area-light geometry
+  const SailSample* samples;
+  float4* accum;            // W x H, row 0 = bottom
+  float4* aovN;             // optional
+  float4* aovP;             // optional
+  unsigned long long* segCounter;  // optional exact segment counter
+  float eye[3];
+  int W, H;
+  int n, tn, ln;
+  uint32_t matMask, texMask, lightMask;
+  int maxBounces;
+  int spp;                  // samples in this launch
+  int accumMode;            // 0 sum, 1 mix, 2 compat8
+  int tilesX, tilesY;       // 64x64 partition tiles of the frame
+  int world, rank;          // tile partition: global tile t belongs to rank t % world
+  int ownedTiles;           // tiles of this rank
+  int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
+};
+
+struct SailFilterArgs {
+  const float4* accum;
+  float4* out;
+  uint8_t* out8;
+  int W, H;
+  int kind;                 // 0 color, 1 gamma, 2 tonemapping, 3 window
+  int accumMode;
+  float invCount;           // unused for mix modes
+  float count;
+  float weights[16];
+  float rx, ry, gammaC;
+};

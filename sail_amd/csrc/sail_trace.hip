@@ -1,0 +1,1086 @@
+// sail_trace.hip — the MI355X (gfx950) trace megakernel and display-filter kernel.
+//
+// Re-implements the per-pixel loop of Sail's generated trace fragment program
+// (src/shader/main/fstrace.glsl:6-17 -> trace/path.glsl:16-38 -> generated intersectObjects /
+// material / light_sample / getSurfaceColor, shader.*.js) and the display pass
+// (main/fsrender.glsl + filter/window.glsl:26-44, tonemapping.glsl, gamma.glsl, color.glsl).
+//
+// MI355X design:
+//  * one lane = one pixel; a 256-thread workgroup covers a 16x16 pixel block, each wave a coherent 16x4 strip;
+//    the grid walks only this rank's 64x64 partition tiles (interleaved t % world);
+//  * all `spp` samples of a launch loop inside the lane with the radiance sum / running mean in
+//    registers: HBM sees one float4 read + one float4 write per pixel per launch;
+//  * the scene is decoded once on the host into 128-B primitive records; the primitive loop index is
+//    wave-uniform, so every record field arrives through the scalar cache into SGPRs (no LDS copy, no
+//    VGPRs), and material/texture/light rows are read with per-lane indices from L1/L2;
+//  * intersectObjects is split into a t-only pass over all primitives and ONE full hit record
+//    (normal, dpdu/dpdv, UV, texture) for the closest primitive; the reference builds the full record
+//    for every primitive hit (shader.shape.js:44-50). The strict-`<`, first-index tie rule and every
+//    f32 operation up to t are kept, so results are bit-identical to the oracle's restatement;
+//  * per-sample camera corners and seeds arrive precomputed (SailSample, scalar loads);
+//  * all f32 math follows the reference expression order with contraction off; transcendentals use
+//    the bit-defined spec in sail_math.h.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sail_device.h"
+#include "sail_math.h"
+
+using namespace sm;
+
+#define D __device__ __forceinline__
+
+namespace {
+
+constexpr float kMaxDistance = 1e5f, kEps = 1e-5f, kOneMinusEps = 0.9999f, kInf = 1e5f;
+constexpr float kPI = 3.141592653589793f, kInvPI = 0.3183098861837907f;
+constexpr float kPiOver2 = 1.570796326794896f, kPiOver4 = 0.785398163397448f;
+
+struct V3 { float x, y, z; };
+struct V2 { float x, y; };
+D V3 v3(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+D V3 v3s(float s) { return v3(s, s, s); }
+D V2 v2(float x, float y) { V2 r; r.x = x; r.y = y; return r; }
+D V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+D V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+D V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+D V3 operator/(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }
+D V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+D V3 operator*(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+D V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+D V3 operator+(V3 a, float s) { return v3(a.x + s, a.y + s, a.z + s); }
+D V3 operator-(V3 a, float s) { return v3(a.x - s, a.y - s, a.z - s); }
+D V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+D V2 operator*(float s, V2 a) { return v2(s * a.x, s * a.y); }
+D float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+D float length(V3 v) { return sqrtf_(dot(v, v)); }
+D V3 normalize(V3 v) { return v / length(v); }
+D V3 vmin(V3 a, V3 b) { return v3(fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)); }
+D V3 vmax(V3 a, V3 b) { return v3(fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)); }
+D V3 vclamp01(V3 x) { return vmin(vmax(x, v3s(0.0f)), v3s(1.0f)); }
+D bool isBlack(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+D V3 reflect_(V3 I, V3 N) { return I - (2.0f * dot(N, I)) * N; }
+D V3 refract_(V3 I, V3 N, float eta) {
+  const float dni = dot(N, I);
+  const float k = 1.0f - eta * eta * (1.0f - dni * dni);
+  if (k < 0.0f) return v3s(0.0f);
+  return eta * I - (eta * dni + sqrtf_(k)) * N;
+}
+D V3 worldToLocal(V3 v, V3 ns, V3 ss, V3 ts) { return v3(dot(v, ss), dot(v, ts), dot(v, ns)); }
+D V3 localToWorld(V3 v, V3 ns, V3 ss, V3 ts) {
+  return v3(ss.x * v.x + ts.x * v.y + ns.x * v.z, ss.y * v.x + ts.y * v.y + ns.y * v.z,
+            ss.z * v.x + ts.z * v.y + ns.z * v.z);
+}
+// OBJECT_SPACE_N/S/T (define.glsl:62-64); kept as full dot products so -0 / NaN propagate like the reference
+D V3 W2L(V3 v) { return worldToLocal(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
+D V3 L2W(V3 v) { return localToWorld(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
+D bool equalZero(float x) { return x < 1e-3f && x > -1e-3f; }
+D float sgn(int rev) { return rev ? -1.0f : 1.0f; }
+
+D bool quadratic(float A, float B, float C, float& t0, float& t1) {  // utility.glsl:37-51
+  const float discrim = B * B - 4.0f * A * C;
+  if (discrim < 0.0f) return false;
+  const float rootDiscrim = sqrtf_(discrim);
+  float q;
+  if (B < 0.0f) q = -0.5f * (B - rootDiscrim);
+  else q = -0.5f * (B + rootDiscrim);
+  t0 = q / A;
+  t1 = C / q;
+  if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
+  return true;
+}
+
+struct Ray { V3 o, d; };
+struct Hit {
+  float d; V3 hit, normal, dpdu, dpdv; bool into; int matRow; V3 sc, emission; int matCategory;
+};
+struct Ctx {
+  const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
+  int n, tn, ln;
+  uint32_t matMask, texMask, lightMask;
+  float fcx, fcy;
+  int shadowAnyHit;
+};
+
+D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
+D float TP(const Ctx& c, int row, int col) { return c.tp[row * 16 + col]; }
+D V3 TP3(const Ctx& c, int row, int col) { return v3(c.tp[row * 16 + col], c.tp[row * 16 + col + 1], c.tp[row * 16 + col + 2]); }
+
+// ---- random.glsl:5-18 ---------------------------------------------------------------------------------
+D float hash1(const Ctx& c, float seed, float a, float b, float cc) {
+  const V3 p = v3(c.fcx + seed, c.fcy + seed, 0.5f + seed);
+  return fract_(sinf_(dot(p, v3(a, b, cc))) * 43758.5453f + seed);
+}
+D V2 random2(const Ctx& c, float seed) {
+  return v2(hash1(c, seed, 12.9898f, 78.233f, 151.7182f), hash1(c, seed, 63.7264f, 10.873f, 623.6736f));
+}
+
+// ---- sampler.glsl ---------------------------------------------------------------------------------------
+D V3 uniformSampleSphere(V2 u) {
+  const float z = 1.0f - 2.0f * u.x;
+  const float r = sqrtf_(1.0f - z * z);
+  const float angle = 2.0f * kPI * u.y;
+  float s, co; sincosf_(angle, s, co);
+  return v3(r * co, r * s, z);
+}
+D V3 cosineSampleHemisphere(V2 u) {
+  const float r = sqrtf_(u.x);
+  const float angle = 2.0f * kPI * u.y;
+  float s, co; sincosf_(angle, s, co);
+  return v3(r * co, r * s, sqrtf_(1.0f - u.x));
+}
+D V2 concentricSampleDisk(V2 u) {
+  const float uOffset = 2.0f * u.x - 1.0f, vOffset = 2.0f * u.y - 1.0f;
+  if (uOffset == 0.0f && vOffset == 0.0f) return v2(0.0f, 0.0f);
+  float theta, r;
+  if (fabsf(uOffset) > fabsf(vOffset)) { r = uOffset; theta = (vOffset / uOffset) * kPiOver4; }
+  else { r = vOffset; theta = kPiOver2 - (uOffset / vOffset) * kPiOver4; }
+  float s, co; sincosf_(theta, s, co);
+  return r * v2(co, s);
+}
+
+// ---- textures (shader.texture.js:22-29) ----------------------------------------------------------------
+D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
+  const int cat = to_int(TP(c, texRow, 0));
+  if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
+  if (cat < 0 || cat >= 32 || !((c.texMask >> cat) & 1u)) return v3s(0.0f);
+  switch (cat) {
+    case SAIL_TEX_CHECKERBOARD: {
+      const float size = TP(c, texRow, 1), lineWidth = TP(c, texRow, 2);
+      const float width = 0.5f * lineWidth / size;
+      const float fx = uv.x / size - floorf(uv.x / size), fy = uv.y / size - floorf(uv.y / size);
+      const bool in_outline = (fx < width || fx > 1.0f - width) || (fy < width || fy > 1.0f - width);
+      return in_outline ? v3s(0.5f) : v3s(1.0f);
+    }
+    case SAIL_TEX_CHECKERBOARD2: {
+      const float size = TP(c, texRow, 7);
+      const float qx = floorf(uv.x / size), qy = floorf(uv.y / size);
+      return (to_int(qx + qy) % 2 == 0) ? TP3(c, texRow, 1) : TP3(c, texRow, 4);
+    }
+    case SAIL_TEX_BILERP: {
+      const V3 c00 = TP3(c, texRow, 1), c01 = TP3(c, texRow, 4), c10 = TP3(c, texRow, 7), c11 = TP3(c, texRow, 10);
+      return (1.0f - uv.x) * (1.0f - uv.y) * c00 + (1.0f - uv.x) * (uv.y) * c01 + (uv.x) * (1.0f - uv.y) * c10 +
+             (uv.x) * (uv.y) * c11;
+    }
+    case SAIL_TEX_MIXF: {
+      const float amount = TP(c, texRow, 7);
+      return (1.0f - amount) * TP3(c, texRow, 1) + amount * TP3(c, texRow, 4);
+    }
+    case SAIL_TEX_SCALE: return TP3(c, texRow, 1) * TP3(c, texRow, 4);
+    case SAIL_TEX_UVF: return v3(uv.x - floorf(uv.x), uv.y - floorf(uv.y), 0.0f);
+    default: return v3s(0.0f);
+  }
+}
+
+// ---- slab boxes: cube.glsl:65-87, cornellbox.glsl:67-90, boundbox.glsl:6-17 ------------------------------
+struct Slab { float tNear, tFar; };
+D Slab slab(V3 bmin, V3 bmax, const Ray& r) {
+  const V3 tMin = (bmin - r.o) / r.d, tMax = (bmax - r.o) / r.d;
+  const V3 t1 = vmin(tMin, tMax), t2 = vmax(tMin, tMax);
+  Slab s;
+  s.tNear = fmax_(fmax_(t1.x, t1.y), t1.z);
+  s.tFar = fmin_(fmin_(t2.x, t2.y), t2.z);
+  return s;
+}
+// Boundbox(max, min) constructor order (boundbox.glsl:1-4): the `min` member is the 2nd argument
+D bool testBoundbox(const Ray& r, V3 bmax, V3 bmin) {
+  const Slab s = slab(bmin, bmax, r);
+  if (s.tNear < 0.0f && s.tFar < 0.0f) return false;
+  return s.tNear < s.tFar;
+}
+D float cubeT(const SailPrim& p, const Ray& r) {
+  const Slab s = slab(P3(p, 0), P3(p, 3), r);
+  float t = -1.0f;
+  if (s.tNear > kEps && s.tNear < s.tFar) t = s.tNear;
+  else if (s.tNear < s.tFar) t = s.tFar;
+  return (t > kEps) ? t : kMaxDistance;
+}
+D float cornellT(const SailPrim& p, const Ray& r) {
+  const Slab s = slab(P3(p, 0), P3(p, 3), r);
+  float t = -1.0f;
+  if (s.tNear < s.tFar) t = s.tFar;
+  return (t > kEps) ? t : kMaxDistance;
+}
+D V3 normalForCube(V3 hit, const SailPrim& p) {  // cube.glsl:25-38
+  const float c = sgn(p.rev);
+  const V3 mn = P3(p, 0), mx = P3(p, 3);
+  if (hit.x < mn.x + 0.0001f) return c * v3(-1.0f, 0.0f, 0.0f);
+  else if (hit.x > mx.x - 0.0001f) return c * v3(1.0f, 0.0f, 0.0f);
+  else if (hit.y < mn.y + 0.0001f) return c * v3(0.0f, -1.0f, 0.0f);
+  else if (hit.y > mx.y - 0.0001f) return c * v3(0.0f, 1.0f, 0.0f);
+  else if (hit.z < mn.z + 0.0001f) return c * v3(0.0f, 0.0f, -1.0f);
+  return c * v3(0.0f, 0.0f, 1.0f);
+}
+D V3 normalForCornellbox(V3 hit, const SailPrim& p) {  // cornellbox.glsl:39-51
+  const V3 mn = P3(p, 0), mx = P3(p, 3);
+  if (hit.x < mn.x + 0.0001f) return v3(-1.0f, 0.0f, 0.0f);
+  else if (hit.x > mx.x - 0.0001f) return v3(1.0f, 0.0f, 0.0f);
+  else if (hit.y < mn.y + 0.0001f) return v3(0.0f, -1.0f, 0.0f);
+  else if (hit.y > mx.y - 0.0001f) return v3(0.0f, 1.0f, 0.0f);
+  else if (hit.z < mn.z + 0.0001f) return v3(0.0f, 0.0f, -1.0f);
+  return v3(0.0f, 0.0f, 1.0f);
+}
+D void dpdBox(V3 normal, V3& dpdu, V3& dpdv) {
+  if (fabsf(normal.x) < 0.5f) dpdu = cross(normal, v3(1.0f, 0.0f, 0.0f));
+  else dpdu = cross(normal, v3(0.0f, 1.0f, 0.0f));
+  dpdv = cross(normal, dpdu);
+}
+D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
+  h.hit = r.o + t * r.d;
+  h.normal = normalForCube(r.o + t * r.d, p);
+  dpdBox(h.normal, h.dpdu, h.dpdv);
+  const V3 mn = P3(p, 0), mx = P3(p, 3);
+  const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
+  V2 uv;
+  if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(hh.y / tr.y, hh.z / tr.z);
+  else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(hh.x / tr.x, hh.z / tr.z);
+  else uv = v2(hh.x / tr.x, hh.y / tr.y);
+  h.sc = getSurfaceColor(c, uv, p.texRow);
+}
+D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
+  h.hit = r.o + t * r.d;
+  h.normal = -normalForCornellbox(r.o + t * r.d, p);
+  dpdBox(h.normal, h.dpdu, h.dpdv);
+  const V3 mn = P3(p, 0), mx = P3(p, 3), x = h.hit;
+  if (x.x < mn.x + 0.0001f) h.sc = v3(0.25f, 0.75f, 0.25f);
+  else if (x.x > mx.x - 0.0001f) h.sc = v3(0.25f, 0.25f, 0.75f);
+  else if (x.y < mn.y + 0.0001f) h.sc = v3s(1.0f);
+  else if (x.y > mx.y - 0.0001f) h.sc = v3s(1.0f);
+  else if (x.z > mn.z + 0.0001f) h.sc = v3s(1.0f);
+  else h.sc = v3s(0.0f);
+}
+
+// ---- sphere.glsl:45-86 ---------------------------------------------------------------------------------------
+D float sphereT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const V3 c = P3(p, 0);
+  const float rad = p.a[3];
+  if (!testBoundbox(r0, c - v3s(rad), c + v3s(rad))) return kMaxDistance;
+  const V3 d = W2L(r0.d), o = W2L(r0.o - c);
+  const float a = dot(d, d), b = 2.0f * dot(o, d), cc = dot(o, o) - rad * rad;
+  float t1 = 0.0f, t2 = 0.0f;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < kEps) return kMaxDistance;
+  float t = t1;
+  if (t1 < kEps) t = t2;
+  if (t >= kMaxDistance) return kMaxDistance;
+  if (hitOut) *hitOut = o + t * d;
+  return t;
+}
+D float phiOf(float y, float x) {
+  float phi = atan2f_(y, x);
+  if (phi < 0.0f) phi += 2.0f * kPI;
+  return phi;
+}
+D V3 dpduRot(V3 hit) { return v3(-2.0f * kPI * hit.y, 2.0f * kPI * hit.x, 0.0f); }
+D void sphereHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hl;
+  const float t = sphereT(p, r, &hl);
+  const float rad = p.a[3];
+  V3 hit = hl;
+  if (hit.x == 0.0f && hit.y == 0.0f) hit.x = 1e-5f * rad;
+  const float phi = phiOf(hit.y, hit.x);
+  const float u = phi / (2.0f * kPI);
+  const float theta = acosf_(clamp_(hit.z / rad, -1.0f, 1.0f));
+  const float v = theta / kPI;
+  (void)t;
+  // computeDpDForSphere (:33-43) on the recomputed (un-guarded) local hit
+  const float th2 = acosf_(clamp_(hl.z / rad, -1.0f, 1.0f));
+  const float zRadius = sqrtf_(hl.x * hl.x + hl.y * hl.y);
+  const float invZRadius = 1.0f / zRadius;
+  const float cosPhi = hl.x * invZRadius, sinPhi = hl.y * invZRadius;
+  const V3 dpdu = dpduRot(hl);
+  const V3 dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(th2));
+  const V3 nl = normalize(cross(dpdv, dpdu));
+  h.sc = getSurfaceColor(c, v2(u, v), p.texRow);
+  h.hit = L2W(hl) + P3(p, 0);
+  h.normal = L2W(nl);
+  h.dpdu = L2W(dpdu);
+  h.dpdv = L2W(dpdv);
+}
+
+// ---- rectangle.glsl:32-63 ---------------------------------------------------------------------------------
+struct RectFrame { V3 dpdu, dpdv, normal, ss, ts; float maxX, maxY; };
+D RectFrame rectFrame(const SailPrim& p) {
+  RectFrame f;
+  const V3 mn = P3(p, 0), mx = P3(p, 3);
+  f.dpdu = v3(mx.x - mn.x, 0.0f, 0.0f);
+  f.dpdv = v3(0.0f, mx.y - mn.y, mx.z - mn.z);
+  f.normal = normalize(cross(f.dpdu, f.dpdv));
+  f.maxX = length(f.dpdu);
+  f.maxY = length(f.dpdv);
+  f.ss = f.dpdu / f.maxX;
+  f.ts = cross(f.normal, f.ss);
+  return f;
+}
+D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
+  const RectFrame f = rectFrame(p);
+  const V3 d = worldToLocal(r.d, f.normal, f.ss, f.ts);
+  const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
+  if (d.z == 0.0f) return kMaxDistance;
+  const float t = -o.z / d.z;
+  if (t < kEps) return kMaxDistance;
+  const V3 hit = o + t * d;
+  if (hit.x > f.maxX || hit.y > f.maxY || hit.x < -kEps || hit.y < -kEps) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+D void rectHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hl;
+  rectT(p, r, &hl);
+  const RectFrame f = rectFrame(p);
+  h.dpdu = f.dpdu; h.dpdv = f.dpdv; h.normal = f.normal;
+  h.sc = getSurfaceColor(c, v2(hl.x / f.maxX, hl.y / f.maxY), p.texRow);
+  h.hit = localToWorld(hl, f.normal, f.ss, f.ts) + P3(p, 0);
+}
+
+// ---- cone.glsl:48-99 / cylinder.glsl:40-90 / hyperboloid.glsl:60-111 / paraboloid.glsl:51-103 ---------------
+// shared tail: two-root retry against the z range, then the MAX_DISTANCE test
+D bool rootPick(float t1, float t2, V3 o, V3 d, float zlo, float zhi, bool epsLo, float& t, V3& hit) {
+  t = t1;
+  if (t1 < kEps) t = t2;
+  hit = o + t * d;
+  const bool out = epsLo ? (hit.z < -kEps || hit.z > zhi) : (hit.z < zlo || hit.z > zhi);
+  if (out) {
+    if (t == t2) return false;
+    t = t2;
+    hit = o + t * d;
+    const bool out2 = epsLo ? (hit.z < -kEps || hit.z > zhi) : (hit.z < zlo || hit.z > zhi);
+    if (out2) return false;
+  }
+  return t < kMaxDistance;
+}
+D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const V3 pp = P3(p, 0);
+  const float h = p.a[3], rad = p.a[4];
+  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  float k = rad / h;
+  k = k * k;
+  const float a = d.x * d.x + d.y * d.y - k * d.z * d.z;
+  const float b = 2.0f * (d.x * o.x + d.y * o.y - k * d.z * (o.z - h));
+  const float cc = o.x * o.x + o.y * o.y - k * (o.z - h) * (o.z - h);
+  float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < -kEps) return kMaxDistance;
+  if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const V3 pp = P3(p, 0);
+  const float h = p.a[3], rad = p.a[4];
+  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  const float a = d.x * d.x + d.y * d.y;
+  const float b = 2.0f * (d.x * o.x + d.y * o.y);
+  const float cc = o.x * o.x + o.y * o.y - rad * rad;
+  float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < -kEps) return kMaxDistance;
+  if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const V3 pp = P3(p, 0), p1 = P3(p, 3), p2 = P3(p, 6);
+  const float ah = p.a[9], ch = p.a[10];
+  {  // testBoundboxForHyperboloid :13-24
+    const float r1 = sqrtf_(p1.x * p1.x + p1.y * p1.y), r2 = sqrtf_(p2.x * p2.x + p2.y * p2.y);
+    const float rMax = fmax_(r1, r2), zMin = fmin_(p1.z, p2.z), zMax = fmax_(p1.z, p2.z);
+    if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
+  }
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  const float a = ah * d.x * d.x + ah * d.y * d.y - ch * d.z * d.z;
+  const float b = 2.0f * (ah * d.x * o.x + ah * d.y * o.y - ch * d.z * o.z);
+  const float cc = ah * o.x * o.x + ah * o.y * o.y - ch * o.z * o.z - 1.0f;
+  float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < -kEps) return kMaxDistance;
+  const float zMin = fmin_(p1.z, p2.z), zMax = fmax_(p1.z, p2.z);
+  if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const V3 pp = P3(p, 0);
+  const float z0 = p.a[3], z1 = p.a[4], rad = p.a[5];
+  const float zMin = fmin_(z0, z1), zMax = fmax_(z0, z1);
+  if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  const float k = zMax / (rad * rad);
+  const float a = k * (d.x * d.x + d.y * d.y);
+  const float b = 2.0f * k * (d.x * o.x + d.y * o.y) - d.z;
+  const float cc = k * (o.x * o.x + o.y * o.y) - o.z;
+  float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < -kEps) return kMaxDistance;
+  if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-75
+  const V3 pp = P3(p, 0);
+  const float rad = p.a[3], ri = p.a[4];
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  if (d.z == 0.0f) return kMaxDistance;
+  const float t = -o.z / d.z;
+  if (t <= 0.0f) return kMaxDistance;
+  const V3 hit = o + t * d;
+  const float dist2 = hit.x * hit.x + hit.y * hit.y;
+  if (dist2 > rad * rad || dist2 < ri * ri) return kMaxDistance;
+  if (t >= kMaxDistance) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
+// local-space tail shared by the quadrics and the disk: normal from dpdu x dpdv, texture, back to world
+D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dpdv, Hit& h) {
+  const V3 nl = normalize(cross(dpdu, dpdv));
+  h.sc = getSurfaceColor(c, uv, p.texRow);
+  h.hit = L2W(hl) + P3(p, 0);
+  h.normal = L2W(nl);
+  h.dpdu = L2W(dpdu);
+  h.dpdv = L2W(dpdv);
+}
+D void coneHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hit; coneT(p, r, &hit);
+  const float hh = p.a[3];
+  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = hit.z / hh;
+  const float vv = hit.z / hh;
+  const V3 dpdv = v3(-hit.x / (1.0f - vv), -hit.y / (1.0f - vv), hh);
+  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), dpdv, h);
+}
+D void cylinderHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hit; cylinderT(p, r, &hit);
+  const float hh = p.a[3];
+  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = hit.z / hh;
+  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), v3(0.0f, 0.0f, hh), h);
+}
+D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperboloid.glsl:41-46
+  float sinPhi, cosPhi; sincosf_(phi, sinPhi, cosPhi);
+  dpdu = dpduRot(hit);
+  dpdv = v3((p2.x - p1.x) * cosPhi - (p2.y - p1.y) * sinPhi, (p2.x - p1.x) * sinPhi + (p2.y - p1.y) * cosPhi, p2.z - p1.z);
+}
+D void hypHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hit; hypT(p, r, &hit);
+  const V3 p1 = P3(p, 3), p2 = P3(p, 6);
+  const float v = (hit.z - p1.z) / (p2.z - p1.z);
+  const V3 pr = (1.0f - v) * p1 + v * p2;
+  const float phi = phiOf(pr.x * hit.y - hit.x * pr.y, hit.x * pr.x + hit.y * pr.y);
+  const float u = phi / (2.0f * kPI);
+  V3 dpdu, dpdv;
+  hypDpD(hit, p1, p2, phi, dpdu, dpdv);
+  finishLocal(c, p, hit, v2(u, v), dpdu, dpdv, h);
+}
+D void paraDpD(V3 hit, float zMax, float zMin, V3& dpdu, V3& dpdv) {  // paraboloid.glsl:35-40
+  dpdu = dpduRot(hit);
+  dpdv = (zMax - zMin) * v3(hit.x / (2.0f * hit.z), hit.y / (2.0f * hit.z), 1.0f);
+}
+D void paraHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hit; paraT(p, r, &hit);
+  const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
+  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = (hit.z - zMin) / (zMax - zMin);
+  V3 dpdu, dpdv;
+  paraDpD(hit, zMax, zMin, dpdu, dpdv);
+  finishLocal(c, p, hit, v2(u, v), dpdu, dpdv, h);
+}
+D void diskHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
+  V3 hit; diskT(p, r, &hit);
+  const float rad = p.a[3], ri = p.a[4];
+  const float dist2 = hit.x * hit.x + hit.y * hit.y;
+  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI);
+  const float rHit = sqrtf_(dist2);
+  const float oneMinusV = ((rHit - ri) / (rad - ri));
+  const float v = 1.0f - oneMinusV;
+  const V3 dpdv = v3(hit.x, hit.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
+  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), dpdv, h);
+}
+
+D float primT(const SailPrim& p, const Ray& r) {
+  switch (p.type) {
+    case SAIL_CUBE: return cubeT(p, r);
+    case SAIL_SPHERE: return sphereT(p, r, nullptr);
+    case SAIL_RECTANGLE: return rectT(p, r, nullptr);
+    case SAIL_CONE: return coneT(p, r, nullptr);
+    case SAIL_CYLINDER: return cylinderT(p, r, nullptr);
+    case SAIL_DISK: return diskT(p, r, nullptr);
+    case SAIL_HYPERBOLOID: return hypT(p, r, nullptr);
+    case SAIL_PARABOLOID: return paraT(p, r, nullptr);
+    case SAIL_CORNELLBOX: return cornellT(p, r);
+    default: return kMaxDistance;
+  }
+}
+
+// closest distance only (shadow rays, testShadow shader.light.js:24-31)
+D float closestT(const Ctx& c, const Ray& r) {
+  float best = kMaxDistance;
+  for (int i = 0; i < c.n; i++) {
+    const float t = primT(c.prims[i], r);
+    if (t < best) {
+      best = t;
+      if (c.shadowAnyHit && best > kEps && best < kOneMinusEps) break;  // exact: no prim returns t <= EPSILON
+    }
+  }
+  return best;
+}
+
+// generated intersectObjects (shader.shape.js:28-51): t-only sweep, then one full record for the winner
+D Hit intersectObjects(const Ctx& c, const Ray& r) {
+  float best = kMaxDistance;
+  int bi = -1;
+  for (int i = 0; i < c.n; i++) {
+    const float t = primT(c.prims[i], r);
+    if (t < best) { best = t; bi = i; }
+  }
+  Hit h;
+  h.d = best;
+  h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
+  h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0;
+  if (bi < 0) return h;
+  const SailPrim& p = c.prims[bi];
+  switch (p.type) {
+    case SAIL_CUBE: cubeHit(c, p, r, best, h); break;
+    case SAIL_SPHERE: sphereHit(c, p, r, h); break;
+    case SAIL_RECTANGLE: rectHit(c, p, r, h); break;
+    case SAIL_CONE: coneHit(c, p, r, h); break;
+    case SAIL_CYLINDER: cylinderHit(c, p, r, h); break;
+    case SAIL_DISK: diskHit(c, p, r, h); break;
+    case SAIL_HYPERBOLOID: hypHit(c, p, r, h); break;
+    case SAIL_PARABOLOID: paraHit(c, p, r, h); break;
+    case SAIL_CORNELLBOX: cornellHit(p, r, best, h); break;
+    default: break;
+  }
+  h.matRow = p.matRow;
+  h.emission = v3(p.em[0], p.em[1], p.em[2]);
+  const V3 nn = sgn(p.rev) * h.normal;                       // faceObj test (shader.shape.js:47-49)
+  if (!(dot(nn, r.d) < -kEps)) h.emission = v3s(0.0f);
+  h.matCategory = to_int(TP(c, h.matRow, 0));
+  h.into = dot(h.normal, r.d) < -kEps;
+  if (!h.into) h.normal = -h.normal;
+  return h;
+}
+
+// ---- sampleGeometry for area lights (shader.shape.js:53-67) -----------------------------------------------------
+D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
+  normal = v3s(0.0f);
+  pdf = 0.0f;
+  const SailPrim& p = c.prims[row];
+  const float s = sgn(p.rev);
+  switch (p.type) {
+    case SAIL_SPHERE: {
+      const V3 q = uniformSampleSphere(u);
+      const float rad = p.a[3];
+      pdf = kInvPI / (rad * rad);
+      const V3 res = q * rad + P3(p, 0);
+      normal = s * (res - P3(p, 0)) / rad;
+      return res;
+    }
+    case SAIL_RECTANGLE: {
+      const V3 mn = P3(p, 0), mx = P3(p, 3);
+      const V3 x = v3(mx.x - mn.x, 0.0f, 0.0f), y = v3(0.0f, mx.y - mn.y, mx.z - mn.z);
+      pdf = 1.0f / (length(x) * length(y));
+      const V3 res = mn + x * u.x + y * u.y;
+      normal = s * normalize(cross(x, y));
+      return res;
+    }
+    case SAIL_DISK: {
+      const V2 pd = concentricSampleDisk(u);
+      const V3 pp = P3(p, 0);
+      const float rad = p.a[3], ri = p.a[4];
+      const V3 res = v3(pd.x * rad + pp.x, pp.y, pd.y * rad + pp.z);
+      const float area = 2.0f * kPI * 0.5f * (rad * rad - ri * ri);
+      pdf = 1.0f / area;
+      normal = s * v3(0.0f, 1.0f, 0.0f);
+      return res;
+    }
+    case SAIL_CUBE: normal = normalForCube(v3s(0.0f), p); return v3s(0.0f);
+    case SAIL_CORNELLBOX: normal = normalForCornellbox(v3s(0.0f), p); return v3s(0.0f);
+    case SAIL_CONE: {  // cone.glsl:38-46 at BLACK
+      const V3 hit = v3s(0.0f) - P3(p, 0);
+      const float h = p.a[3], rad = p.a[4];
+      const float tana = rad / h;
+      const float dd = sqrtf_(hit.x * hit.x + hit.y * hit.y);
+      const float x1 = dd / tana, x2 = dd * tana;
+      normal = s * normalize(hit - v3(0.0f, 0.0f, h - x1 - x2));
+      return v3s(0.0f);
+    }
+    case SAIL_CYLINDER: {
+      const V3 pp = P3(p, 0);
+      normal = s * normalize(v3(0.0f - pp.x, 0.0f - pp.y, 0.0f));
+      return v3s(0.0f);
+    }
+    case SAIL_HYPERBOLOID: {
+      const V3 hit = v3s(0.0f), p1 = P3(p, 3), p2 = P3(p, 6);
+      const float v = (hit.z - p1.z) / (p2.z - p1.z);
+      const V3 pr = (1.0f - v) * p1 + v * p2;
+      const float phi = phiOf(pr.x * hit.y - hit.x * pr.y, hit.x * pr.x + hit.y * pr.y);
+      V3 dpdu, dpdv;
+      hypDpD(hit, p1, p2, phi, dpdu, dpdv);
+      normal = s * L2W(normalize(cross(dpdu, dpdv)));
+      return v3s(0.0f);
+    }
+    case SAIL_PARABOLOID: {
+      const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
+      V3 dpdu, dpdv;
+      paraDpD(v3s(0.0f), zMax, zMin, dpdu, dpdv);
+      normal = s * L2W(normalize(cross(dpdu, dpdv)));
+      return v3s(0.0f);
+    }
+    default: return v3s(0.0f);
+  }
+}
+
+// ---- ssutility.glsl / fresnel.glsl / microfacet.glsl / bsdf.glsl --------------------------------------------------
+D float absCosTheta(V3 w) { return fabsf(w.z); }
+D float sin2Theta(V3 w) { return fmax_(0.0f, 1.0f - w.z * w.z); }
+D float sinTheta(V3 w) { return sqrtf_(sin2Theta(w)); }
+D float tan2Theta(V3 w) {
+  const float cos2T = w.z * w.z;
+  if (cos2T < kEps) return kInf;
+  return sin2Theta(w) / cos2T;
+}
+D float cosPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 1.0f : clamp_(w.x / st, -1.0f, 1.0f); }
+D float sinPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 0.0f : clamp_(w.y / st, -1.0f, 1.0f); }
+D bool sameHemisphere(V3 w, V3 wp) { return w.z * wp.z > kEps; }
+
+D float frDielectric(float cosThetaI, float etaI, float etaT) {
+  cosThetaI = clamp_(cosThetaI, -1.0f, 1.0f);
+  const float sinThetaI = sqrtf_(fmax_(0.0f, 1.0f - cosThetaI * cosThetaI));
+  const float sinThetaT = etaI / etaT * sinThetaI;
+  if (sinThetaT >= 1.0f) return 1.0f;
+  const float cosThetaT = sqrtf_(fmax_(0.0f, 1.0f - sinThetaT * sinThetaT));
+  const float TI = etaT * cosThetaI, IT = etaI * cosThetaT, II = etaI * cosThetaI, TT = etaT * cosThetaT;
+  const float Rparl = (TI - IT) / (TI + IT), Rperp = (II - TT) / (II + TT);
+  return (Rparl * Rparl + Rperp * Rperp) / 2.0f;
+}
+D V3 frConductor(float cosThetaI, V3 etaI, V3 etaT, V3 k) {
+  cosThetaI = clamp_(cosThetaI, -1.0f, 1.0f);
+  const V3 eta = etaT / etaI, etak = k / etaI;
+  const float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1.0f - cosThetaI2;
+  const V3 eta2 = eta * eta, etak2 = etak * etak;
+  const V3 t0 = eta2 - etak2 - sinThetaI2;
+  const V3 s = t0 * t0 + 4.0f * eta2 * etak2;
+  const V3 a2plusb2 = v3(sqrtf_(s.x), sqrtf_(s.y), sqrtf_(s.z));
+  const V3 t1 = a2plusb2 + cosThetaI2;
+  const V3 ah = 0.5f * (a2plusb2 + t0);
+  const V3 a = v3(sqrtf_(ah.x), sqrtf_(ah.y), sqrtf_(ah.z));
+  const V3 t2 = 2.0f * cosThetaI * a;
+  const V3 Rs = (t1 - t2) / (t1 + t2);
+  const V3 t3 = cosThetaI2 * a2plusb2 + v3s(sinThetaI2 * sinThetaI2);
+  const V3 t4 = t2 * sinThetaI2;
+  const V3 Rp = Rs * (t3 - t4) / (t3 + t4);
+  return 0.5f * (Rp + Rs);
+}
+// Fresnel: type 0 noop (WHITE), 1 conductor(etaI=WHITE, eta, k), 2 dielectric(1, eta)
+struct Fr { int type; V3 eta, k; float etaT; };
+D V3 frEvaluate(const Fr& f, float cosThetaI) {
+  if (f.type == 2) return v3s(1.0f) * frDielectric(cosThetaI, 1.0f, f.etaT);
+  else if (f.type == 1) return frConductor(cosThetaI, v3s(1.0f), f.eta, f.k);
+  return v3s(1.0f);
+}
+D V3 trSampleWh(V2 u, float ax, float ay, V3 wo) {  // microfacet.glsl:41-59
+  float cosT = 0.0f, phi = 2.0f * kPI * u.x;
+  if (ax == ay) {
+    const float tanTheta2 = ax * ax * u.x / (1.0f - u.x);
+    cosT = 1.0f / sqrtf_(1.0f + tanTheta2);
+  } else {
+    phi = atanf_(ay / ax * tanf_(kPiOver2 + 2.0f * kPI * u.x));
+    if (u.x > 0.5f) phi += kPI;
+    float sP, cP; sincosf_(phi, sP, cP);
+    const float ax2 = ax * ax, ay2 = ay * ay;
+    const float alpha2 = 1.0f / (cP * cP / ax2 + sP * sP / ay2);
+    const float tanTheta2 = alpha2 * u.x / (1.0f - u.x);
+    cosT = 1.0f / sqrtf_(1.0f + tanTheta2);
+  }
+  const float sinT = sqrtf_(fmax_(0.0f, 1.0f - cosT * cosT));
+  float sp, cp; sincosf_(phi, sp, cp);
+  V3 wh = v3(sinT * cp, sinT * sp, cosT);
+  if (!sameHemisphere(wo, wh)) wh = -wh;
+  return wh;
+}
+D float trD(float ax, float ay, V3 wh) {  // microfacet.glsl:61-67
+  const float t2 = tan2Theta(wh);
+  if (t2 >= kInf) return 0.001f;
+  const float c2 = wh.z * wh.z;
+  const float cos4Theta = c2 * c2;
+  const float cp = cosPhi(wh), sp = sinPhi(wh);
+  const float e = (cp * cp / (ax * ax) + sp * sp / (ay * ay)) * t2;
+  return 1.0f / (kPI * ax * ay * cos4Theta * (1.0f + e) * (1.0f + e));
+}
+D float trPdf(float ax, float ay, V3 wh) { return trD(ax, ay, wh) * absCosTheta(wh); }
+D V3 microR_f(V3 R, const Fr& fr, float ax, float ay, V3 wo, V3 wi) {  // bsdf.glsl:168-178
+  const float cosThetaO = absCosTheta(wo), cosThetaI = absCosTheta(wi);
+  V3 wh = wi + wo;
+  if (cosThetaI < kEps || cosThetaO < kEps) return v3s(0.0f);
+  if (equalZero(wh.x) && equalZero(wh.y) && equalZero(wh.z)) return v3s(0.0f);
+  wh = normalize(wh);
+  const V3 F = frEvaluate(fr, dot(wi, wh));
+  return R * trD(ax, ay, wh) * F / (4.0f * cosThetaI * cosThetaO);
+}
+D V3 microR_sample(V3 R, const Fr& fr, float ax, float ay, V2 u, V3 wo, V3& wi, float& pdf) {  // :186-196
+  if (wo.z < kEps) return v3s(0.0f);
+  const V3 wh = trSampleWh(u, ax, ay, wo);
+  wi = reflect_(-wo, wh);
+  if (!sameHemisphere(wo, wi)) return v3s(0.0f);
+  pdf = trPdf(ax, ay, wh) / (4.0f * dot(wo, wh));
+  return microR_f(R, fr, ax, ay, wo, wi);
+}
+D V3 microT_f(V3 T, float etaB, bool into, float ax, float ay, V3 wo, V3 wi) {  // :205-224 (etaA = 1)
+  if (sameHemisphere(wo, wi)) return v3s(0.0f);
+  const float cosThetaO = wo.z, cosThetaI = wi.z;
+  if (equalZero(cosThetaI) || equalZero(cosThetaO)) return v3s(0.0f);
+  const float eta = into ? (etaB / 1.0f) : (1.0f / etaB);
+  V3 wh = normalize(wo + wi * eta);
+  if (wh.z < -kEps) wh = -wh;
+  const float Fd = frDielectric(dot(wo, wh), 1.0f, etaB);
+  const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+  return (1.0f - Fd) * T *
+         fabsf(eta * eta * trD(ax, ay, wh) * fabsf(dot(wi, wh)) * fabsf(dot(wo, wh)) /
+               (cosThetaI * cosThetaO * sqrtDenom * sqrtDenom));
+}
+D float microT_pdf(float etaB, bool into, float ax, float ay, V3 wo, V3 wi) {  // :226-235
+  if (sameHemisphere(wo, wi)) return 0.001f;
+  const float eta = into ? (etaB / 1.0f) : (1.0f / etaB);
+  const V3 wh = normalize(wo + wi * eta);
+  const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+  const float dwh_dwi = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
+  return trPdf(ax, ay, wh) * dwh_dwi;
+}
+D V3 microT_sample(V3 T, float etaB, bool into, float ax, float ay, V2 u, V3 wo, V3& wi, float& pdf) {
+  if (equalZero(wo.z)) return v3s(0.0f);
+  const V3 wh = trSampleWh(u, ax, ay, wo);
+  const float eta = into ? (1.0f / etaB) : (etaB / 1.0f);
+  wi = refract_(-wo, wh, eta);
+  pdf = microT_pdf(etaB, into, ax, ay, wo, wi);
+  return microT_f(T, etaB, into, ax, ay, wo, wi);
+}
+D V3 orenNayar_f(V3 R, float A, float B, V3 wo, V3 wi) {  // bsdf.glsl:45-66
+  const float sinThetaI = sinTheta(wi), sinThetaO = sinTheta(wo);
+  float maxCos = 0.0f;
+  if (sinThetaI > kEps && sinThetaO > kEps) {
+    const float sinPhiI = sinPhi(wi), cosPhiI = cosPhi(wi), sinPhiO = sinPhi(wo), cosPhiO = cosPhi(wo);
+    const float dCos = cosPhiI * cosPhiO + sinPhiI * sinPhiO;
+    maxCos = fmax_(0.0f, dCos);
+  }
+  float sinAlpha, tanBeta;
+  if (absCosTheta(wi) > absCosTheta(wo)) { sinAlpha = sinThetaO; tanBeta = sinThetaI / absCosTheta(wi); }
+  else { sinAlpha = sinThetaI; tanBeta = sinThetaO / absCosTheta(wo); }
+  return R * kInvPI * (A + B * maxCos * sinAlpha * tanBeta);
+}
+
+// material() (shader.material.js:21-29): returns fpdf; f only for MATTE (the only consumer, path.glsl:10-11)
+D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
+  f = v3s(0.0f);
+  wi = v3s(0.0f);
+  const int cat = ins.matCategory;
+  if (cat < 0 || cat >= 32 || !((c.matMask >> cat) & 1u)) return v3s(0.0f);
+  const int m = ins.matRow;
+  const V3 sc = ins.sc;
+  float pdf = 0.0f;
+  V3 fs = v3s(0.0f);
+  switch (cat) {
+    case SAIL_MATTE: {  // matte.glsl:8-37
+      const float kd = TP(c, m, 1), sigma = TP(c, m, 2), A = TP(c, m, 3), B = TP(c, m, 4);
+      const V3 R = kd * sc;
+      wi = cosineSampleHemisphere(u);
+      pdf = sameHemisphere(wo, wi) ? absCosTheta(wi) * kInvPI : 0.0f;
+      if (sigma < kEps) { fs = R * kInvPI; f = (kd * sc) * kInvPI; }
+      else { fs = orenNayar_f(R, A, B, wo, wi); f = orenNayar_f(kd * sc, A, B, wo, wi); }
+      break;
+    }
+    case SAIL_MIRROR: {  // mirror.glsl:5-17, specular_r_sample_f bsdf.glsl:93-98
+      const float kr = TP(c, m, 1);
+      const V3 R = kr * sc;
+      wi = v3(-wo.x, -wo.y, wo.z);
+      pdf = 1.0f;
+      fs = v3s(1.0f) * R / absCosTheta(wi);
+      break;
+    }
+    case SAIL_METAL: {  // metal.glsl:8-22
+      Fr fr; fr.type = 1; fr.eta = TP3(c, m, 3); fr.k = TP3(c, m, 6); fr.etaT = 0.0f;
+      fs = microR_sample(sc, fr, TP(c, m, 1), TP(c, m, 2), u, wo, wi, pdf);
+      break;
+    }
+    case SAIL_GLASS: {  // glass.glsl:10-36
+      const float kr = TP(c, m, 1), kt = TP(c, m, 2), eta = TP(c, m, 3), ur = TP(c, m, 4), vr = TP(c, m, 5);
+      if (ur < kEps && vr < kEps) {  // specular_fr_sample_f bsdf.glsl:141-158
+        const float Fd = frDielectric(wo.z, 1.0f, eta);
+        if (u.x < Fd) {
+          wi = v3(-wo.x, -wo.y, wo.z);
+          pdf = 1.0f;
+          fs = (kr * sc) / absCosTheta(wi);
+        } else {
+          const float etaI = ins.into ? 1.0f : eta, etaT = ins.into ? eta : 1.0f;
+          wi = refract_(-wo, v3(0.0f, 0.0f, 1.0f), etaI / etaT);
+          const V3 ft = (kt * sc) * (1.0f - Fd);
+          pdf = 1.0f;
+          fs = ft / absCosTheta(wi);
+        }
+      } else {
+        const float p = u.x;
+        V2 uu = u;
+        uu.x = fmin_(u.x * 2.0f - 1.0f, kOneMinusEps);
+        if (p < 0.5f) {
+          Fr fr; fr.type = 2; fr.etaT = eta; fr.eta = v3s(0.0f); fr.k = v3s(0.0f);
+          fs = microR_sample(kr * sc, fr, ur, vr, uu, wo, wi, pdf);
+        } else {
+          fs = microT_sample(kt * sc, eta, ins.into, ur, vr, uu, wo, wi, pdf);
+        }
+      }
+      break;
+    }
+    default: break;
+  }
+  return fs * absCosTheta(wi) / pdf;
+}
+
+// ---- lights (shader.light.js:12-22, light/*.glsl) ---------------------------------------------------------------
+D bool testShadow(const Ctx& c, const Ray& r) {
+  const float d = closestT(c, r);
+  return d > kEps && d < kOneMinusEps;
+}
+D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
+  // randomInt(seed,0,ln) = int(random2(seed).x * ln): the same hash as the BSDF sample's first component
+  const int index = to_int(u2.x * (float)c.ln);
+  if (c.ln <= 0) return v3s(0.0f);
+  const int catRow = (index <= 0) ? 0 : c.ln - 1;           // readInt(lights, vec2(0, index)) : integer row coord
+  const int cat = to_int(c.lt[catRow * 18]);
+  if (cat < 0 || cat >= 32 || !((c.lightMask >> cat) & 1u)) return v3s(0.0f);
+  const int row = (c.ln == 1) ? 0 : (index < 0 ? 0 : (index > c.ln - 1 ? c.ln - 1 : index));
+  const float* L = c.lt + row * 18;
+  if (cat == SAIL_AREA) {
+    const V3 em = v3(L[2], L[3], L[4]);
+    V3 normal; float pdf;
+    const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
+    const V3 toLight = p - ins.hit;
+    const V3 nt = normalize(toLight);
+    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    if (testShadow(c, sr)) return v3s(0.0f);
+    return em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
+  } else if (cat == SAIL_POINT) {
+    const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
+    const V3 p = from + uniformSampleSphere(u2) * 0.1f;
+    const V3 toLight = p - ins.hit;
+    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    if (testShadow(c, sr)) return v3s(0.0f);
+    return em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
+  } else if (cat == SAIL_SPOT) {
+    const float ctw = L[1], cfs = L[2];
+    const V3 from = v3(L[3], L[4], L[5]), em = v3(L[6], L[7], L[8]);
+    const V3 toLight = from - ins.hit;
+    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    if (testShadow(c, sr)) return v3s(0.0f);
+    const V3 nt = normalize(toLight);
+    const float d = length(toLight);
+    float fall;
+    {  // falloff spot.glsl:17-27 with w = -normToLight
+      const float cT = -(-nt).y;
+      if (cT < ctw) fall = 0.0f;
+      else if (cT >= cfs) fall = 1.0f;
+      else { const float delta = (cT - ctw) / (cfs - ctw); const float d2 = delta * delta; fall = d2 * d2; }
+    }
+    return em * fall * fmax_(0.0f, dot(normalize(toLight), ins.normal)) / (d * d);
+  }
+  return v3s(0.0f);
+}
+
+// ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
+D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigned& segs) {
+  V3 fpdf = v3s(1.0f), e = v3s(0.0f);
+  for (int depth = 1; depth <= maxDepth; depth++) {
+    segs++;
+    const Hit ins = intersectObjects(c, ray);
+    const float seed = tss + (float)depth;
+    if (ins.d >= kMaxDistance) break;
+    if (depth == 1) { n = ins.normal; p = ins.hit; }
+    // shade()
+    const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
+    const V3 wo = worldToLocal(-ray.d, ins.normal, ss, ts);
+    const V2 u2 = random2(c, seed);
+    V3 wiL, f;
+    const V3 mat = material(c, ins, u2, wo, wiL, f);
+    const V3 _fpdf = vclamp01(mat);
+    const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
+    V3 direct = v3s(0.0f);
+    if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) direct = direct + lightSample(c, ins, u2) * f;
+    const V3 sh = ins.emission + direct;
+    e = e + sh * fpdf;
+    fpdf = fpdf * _fpdf;
+    const float outdot = dot(ins.normal, wi);
+    ray.o = ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f);
+    ray.d = wi;
+  }
+  return e;
+}
+
+D float q8(float v) {
+  v = fmin_(fmax_(v, 0.0f), 1.0f);
+  return floorf(v * 255.0f + 0.5f) / 255.0f;
+}
+
+}  // namespace
+
+// 256 threads = 16x16 pixel block; wave w covers the 16x4 strip rows 4w..4w+3; 16 blocks per 64x64 tile.
+extern "C" __global__ void __launch_bounds__(256) sail_trace_kernel(SailTraceArgs A) {
+  const int ownedTile = blockIdx.x >> 4;
+  const int sub = blockIdx.x & 15;
+  const int tile = A.rank + ownedTile * A.world;
+  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int x = tx * 64 + (sub & 3) * 16 + (lane & 15);
+  const int y = ty * 64 + (sub >> 2) * 16 + wave * 4 + (lane >> 4);
+  if (x >= A.W || y >= A.H || ownedTile >= A.ownedTiles) return;
+
+  Ctx c;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.prims = A.prims;
+  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
+  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
+  c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
+  c.shadowAnyHit = A.shadowAnyHit;
+
+  const size_t pix = (size_t)y * A.W + x;
+  float4 acc = A.accum[pix];
+  const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
+  const bool tri0 = s + t <= 1.0f;
+  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
+  V3 nAov = v3s(0.0f), pAov = v3s(0.0f);
+  unsigned segs = 0;
+  for (int k = 0; k < A.spp; k++) {
+    const SailSample& S = A.samples[k];
+    const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
+    const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
+    Ray ray;
+    ray.o = eye;
+    ray.d = tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t));
+    nAov = v3s(0.0f); pAov = v3s(0.0f);
+    const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs);
+    if (A.accumMode == 0) {
+      acc.x += e.x; acc.y += e.y; acc.z += e.z; acc.w += 1.0f;
+    } else {
+      const float w = S.mixw;
+      float mx = e.x * (1.0f - w) + acc.x * w, my = e.y * (1.0f - w) + acc.y * w, mz = e.z * (1.0f - w) + acc.z * w;
+      if (A.accumMode == 2) { mx = q8(mx); my = q8(my); mz = q8(mz); }
+      acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
+    }
+  }
+  A.accum[pix] = acc;
+  if (A.aovN) {
+    const V3 q = nAov / 2.0f + 0.5f;
+    A.aovN[pix] = make_float4(q.x, q.y, q.z, 1.0f);
+  }
+  if (A.aovP) {
+    const V3 q = normalize(pAov);
+    A.aovP[pix] = make_float4(q.x, q.y, q.z, 1.0f);
+  }
+  if (A.segCounter) {
+    // one atomic per wave: sum the lanes' segment counts with a cross-lane reduction
+    unsigned long long v = segs;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) atomicAdd(A.segCounter, v);
+  }
+}
+
+// ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
+namespace {
+D int wrapi(int i, int size) { int m = i % size; return m < 0 ? m + size : m; }
+D float meanC(const SailFilterArgs& A, int xi, int yi, int ch) {
+  const float4 v = A.accum[(size_t)yi * A.W + xi];
+  const float comp = ch == 0 ? v.x : (ch == 1 ? v.y : v.z);
+  return A.accumMode == 0 ? comp / A.count : comp;
+}
+D void bilinear(const SailFilterArgs& A, float u, float v, float out[3]) {
+  const float fx = u * (float)A.W - 0.5f, fy = v * (float)A.H - 0.5f;
+  const float x0f = floorf(fx), y0f = floorf(fy);
+  const float a = fx - x0f, b = fy - y0f;
+  const int xi = (int)x0f, yi = (int)y0f;
+  const int xa = wrapi(xi, A.W), xb = wrapi(xi + 1, A.W), ya = wrapi(yi, A.H), yb = wrapi(yi + 1, A.H);
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const float t00 = meanC(A, xa, ya, c), t10 = meanC(A, xb, ya, c), t01 = meanC(A, xa, yb, c), t11 = meanC(A, xb, yb, c);
+    const float c0 = t00 * (1.0f - a) + t10 * a, c1 = t01 * (1.0f - a) + t11 * a;
+    out[c] = c0 * (1.0f - b) + c1 * b;
+  }
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterArgs A) {
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= A.W || y >= A.H) return;
+  const float tcx = ((float)x + 0.5f) / (float)A.W, tcy = ((float)y + 0.5f) / (float)A.H;
+  float o[3];
+  if (A.kind == 0 || A.kind == 1 || A.kind == 2) {
+    float col[3];
+    bilinear(A, tcx, tcy, col);
+    for (int c = 0; c < 3; c++) {
+      if (A.kind == 0) o[c] = col[c];
+      else if (A.kind == 1) o[c] = powf_(col[c], 1.0f / A.gammaC);
+      else {
+        const float xx = fmax_(0.0f, col[c] - 0.004f);
+        o[c] = (xx * (6.2f * xx + 0.5f)) / (xx * (6.2f * xx + 1.7f) + 0.06f);
+      }
+    }
+  } else {
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    float weightSum = 0.0f;
+    for (int i = 0; i < 4; i++) {
+      for (int j = 0; j < 4; j++) {
+        const float wi = ((float)j + 0.5f) * A.rx / 4.0f, wj = ((float)i + 0.5f) * A.ry / 4.0f;
+        const float ox = wi / (float)A.W, oy = wj / (float)A.H;
+        float tmp[3] = {0.0f, 0.0f, 0.0f};
+        int count = 0;
+        for (int q = 0; q < 4; q++) {
+          const float u = (q < 2) ? tcx + ox : tcx - ox;
+          const float v = (q & 1) ? tcy - oy : tcy + oy;
+          if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) continue;
+          count++;
+          float s3[3];
+          bilinear(A, u, v, s3);
+          tmp[0] += s3[0]; tmp[1] += s3[1]; tmp[2] += s3[2];
+        }
+        const float weight = A.weights[i * j + j];
+        weightSum += weight * (float)count;
+        acc[0] += tmp[0] * weight; acc[1] += tmp[1] * weight; acc[2] += tmp[2] * weight;
+      }
+    }
+    o[0] = acc[0] / weightSum; o[1] = acc[1] / weightSum; o[2] = acc[2] / weightSum;
+  }
+  const size_t pix = (size_t)y * A.W + x;
+  if (A.out) A.out[pix] = make_float4(o[0], o[1], o[2], 1.0f);
+  if (A.out8) {
+    for (int c = 0; c < 3; c++) A.out8[4 * pix + c] = (uint8_t)(int)(fmin_(fmax_(o[c], 0.0f), 1.0f) * 255.0f + 0.5f);
+    A.out8[4 * pix + 3] = 255;
+  }
+}
+
+// ---- spec-math probe for the CPU/GPU bit-parity test ----------------------------------------------------------------
+extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float* y, float* out, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float r = 0.0f;
+  switch (fn) {
+    case 0: r = sinf_(x[i]); break;
+    case 1: r = cosf_(x[i]); break;
+    case 2: r = tanf_(x[i]); break;
+    case 3: r = atan2f_(y[i], x[i]); break;
+    case 4: r = acosf_(x[i]); break;
+    case 5: r = powf_(x[i], y[i]); break;
+    case 6: r = atanf_(x[i]); break;
+    case 7: r = sqrtf_(x[i]); break;
+    case 8: r = x[i] / y[i]; break;
+    default: break;
+  }
+  out[i] = r;
+}
+
+// ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
+hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s) {
+  hipLaunchKernelGGL(sail_filter_kernel, dim3((A.W + 15) / 16, (A.H + 15) / 16), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count) {
+  hipLaunchKernelGGL(sail_math_kernel, dim3((count + 255) / 256), dim3(256), 0, 0, fn, x, y, out, count);
+  return hipGetLastError();
+}
