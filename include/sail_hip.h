@@ -120,6 +120,9 @@ int sail_comm_unique_id(char id[128]);
 int sail_comm_init(sail_ctx* ctx, const char id[128], int nranks, int rank);
 int sail_reduce(sail_ctx* ctx, int root);                /* in-place sum of the float4 accumulators into root */
 int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes); /* for an external collective */
+/* the 64x64 tiles rank `rank` of `world` owns in a W x H frame (tile t -> rank t % world), as
+ * (x0, y0, w, h) quadruples; returns the tile count (or a negative error); out may be NULL to count */
+int sail_partition_tiles(int width, int height, int rank, int world, int* out_xywh, int capacity);
 
 /* ---- diagnostics ---- */
 /* evaluate the build's f32 math spec on the device (fn: 0 sin 1 cos 2 tan 3 atan2(y,x) 4 acos 5 pow(x,y)

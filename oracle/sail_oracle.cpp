@@ -1412,3 +1412,35 @@ float oracle_intersect_t(const float* objects, int n, const float* texparams, in
 }
 
 }  // extern "C"
+
+// ---- unit probes of individual restated functions (known-answer tests) ----------------------------------------
+extern "C" int oracle_probe(int fn, const float* in, float* out) {
+  switch (fn) {
+    case 0: out[0] = raw(frDielectric(F(in[0]), F(in[1]), F(in[2]))); return 0;
+    case 1: {
+      const V3 r = frConductor(F(in[0]), WHITEv, v3(F(in[1]), F(in[2]), F(in[3])), v3(F(in[4]), F(in[5]), F(in[6])));
+      out[0] = raw(r.x); out[1] = raw(r.y); out[2] = raw(r.z); return 0;
+    }
+    case 2: {
+      F t0 = F(0.0f), t1 = F(0.0f);
+      const bool ok = quadratic(F(in[0]), F(in[1]), F(in[2]), t0, t1);
+      out[0] = ok ? 1.0f : 0.0f; out[1] = raw(t0); out[2] = raw(t1); return 0;
+    }
+    case 3: { const V3 r = cosineSampleHemisphere(v2(F(in[0]), F(in[1]))); out[0] = raw(r.x); out[1] = raw(r.y); out[2] = raw(r.z); return 0; }
+    case 4: out[0] = raw(trD(F(in[0]), F(in[1]), v3(F(in[2]), F(in[3]), F(in[4])))); return 0;
+    case 5: {
+      C.fcx = F(in[1]); C.fcy = F(in[2]); C.fcz = F(0.5f);
+      const V2 r = random2(F(in[0])); out[0] = raw(r.x); out[1] = raw(r.y); return 0;
+    }
+    case 6: { const V2 r = concentricSampleDisk(v2(F(in[0]), F(in[1]))); out[0] = raw(r.x); out[1] = raw(r.y); return 0; }
+    case 7: { const V3 r = uniformSampleSphere(v2(F(in[0]), F(in[1]))); out[0] = raw(r.x); out[1] = raw(r.y); out[2] = raw(r.z); return 0; }
+    case 8: {  // Lambert matte throughput f*|cos|/pdf for R = in[0..2], wo = (0,0,1), u = in[3..4]
+      const V3 R = v3(F(in[0]), F(in[1]), F(in[2]));
+      const V3 wi = cosineSampleHemisphere(v2(F(in[3]), F(in[4])));
+      const F pdf = sameHemisphere(v3(F(0.0f), F(0.0f), F(1.0f)), wi) ? absCosTheta(wi) * F(kInvPI) : F(0.0f);
+      const V3 r = (R * F(kInvPI)) * absCosTheta(wi) / pdf;
+      out[0] = raw(r.x); out[1] = raw(r.y); out[2] = raw(r.z); return 0;
+    }
+    default: return -1;
+  }
+}

@@ -28,7 +28,8 @@ EXPORTS = (
     "sail_update_objects", "sail_set_accum_mode", "sail_set_partition", "sail_set_launch_samples",
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
-    "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_math_probe",
+    "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
+    "sail_math_probe",
     "sail_abi_version",
 )
 
@@ -106,6 +107,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_comm_init": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
         "sail_reduce": (ctypes.c_int, [vp, ctypes.c_int]),
         "sail_accum_device_ptr": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]),
+        "sail_partition_tiles": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
         "sail_math_probe": (ctypes.c_int, [ctypes.c_int, f32p, f32p, f32p, ctypes.c_int]),
         "sail_abi_version": (ctypes.c_int, []),
     }
@@ -160,6 +163,17 @@ def schedule(mvp: np.ndarray, width: int, height: int, k0: int, spp: int):
     if rc:
         raise SailError(f"sail_schedule: {rc}")
     return inv, seeds
+
+
+def partition_tiles(width: int, height: int, rank: int, world: int) -> np.ndarray:
+    """(x0, y0, w, h) of the 64x64 tiles a rank owns (tile t -> rank t % world)."""
+    lib = load()
+    n = lib.sail_partition_tiles(width, height, rank, world, ctypes.cast(None, ctypes.POINTER(ctypes.c_int)), 0)
+    if n < 0:
+        raise SailError(f"sail_partition_tiles: {n}")
+    out = np.zeros((max(n, 1), 4), dtype=np.int32)
+    lib.sail_partition_tiles(width, height, rank, world, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), n)
+    return out[:n]
 
 
 def math_probe(fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:

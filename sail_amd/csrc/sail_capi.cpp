@@ -625,6 +625,23 @@ int sail_reduce(sail_ctx* c, int root) {
   return SAIL_OK;
 }
 
+int sail_partition_tiles(int width, int height, int rank, int world, int* out, int capacity) {
+  if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || capacity < 0) return SAIL_E_INVALID;
+  const int tx = (width + 63) / 64, ty = (height + 63) / 64;
+  int count = 0;
+  for (int t = rank; t < tx * ty; t += world) {
+    if (out && count < capacity) {
+      const int x0 = (t % tx) * 64, y0 = (t / tx) * 64;
+      out[4 * count + 0] = x0;
+      out[4 * count + 1] = y0;
+      out[4 * count + 2] = (width - x0) < 64 ? (width - x0) : 64;
+      out[4 * count + 3] = (height - y0) < 64 ? (height - y0) : 64;
+    }
+    count++;
+  }
+  return count;
+}
+
 int sail_math_probe(int fn, const float* x, const float* y, float* out, int count) {
   if (!x || !y || !out || count < 0) return SAIL_E_INVALID;
   if (count == 0) return SAIL_OK;
