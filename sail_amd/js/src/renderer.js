@@ -1,0 +1,134 @@
+'use strict';
+// Sail.Renderer over libsail_hip.so (through the N-API addon) in place of the WebGL2 programs.
+//   new Renderer(canvas | {width, height, device, ...})   src/core/renderer.js:9-39
+//   renderer.update(scene)        -> Tracer.update (tracer.js:42-90): rows + plugin set -> sail_set_scene
+//   renderer.updateObjects(scene) -> Tracer.updateObjects (tracer.js:25-40) -> sail_update_objects
+//   renderer.render(scene)        -> Tracer.render (tracer.js:92-101): one progressive sample with a
+//                                    jittered inverse camera matrix and a time seed -> sail_render, then the
+//                                    display filter (renderer.js:63) -> sail_filter, painted to the canvas
+// Extensions (same API object): renderSamples(scene, spp) runs a whole deterministic sample schedule in
+// one call; readPixels() / readAOV() / image() read the float frame back (the reference never reads back).
+const native = require('./native');
+const { filterConfig } = require('./filter');
+
+const MAXBOUNCES = 5;  // define.glsl:6
+const ACCUM = { sum: 0, mix: 1, compat8: 2 };
+const SHAPE_ID = { cube: 1, sphere: 2, rectangle: 3, cone: 4, cylinder: 5, disk: 6, hyperboloid: 7, paraboloid: 8, cornellbox: 9 };
+const MAT_ID = { matte: 1, mirror: 2, metal: 3, glass: 4 };
+const TEX_ID = { checkerboard: 5, checkerboard2: 7, bilerp: 8, mixf: 9, scale: 10, uvf: 11 };
+const LIGHT_ID = { area: 0, point: 1, spot: 2 };
+
+function masksOf(cfg) {
+  const m = (list, table) => list.reduce((acc, p) => acc | (1 << table[p.name]), 0) >>> 0;
+  return [m(cfg.shape, SHAPE_ID), m(cfg.material, MAT_ID), m(cfg.texture, TEX_ID), m(cfg.light, LIGHT_ID)];
+}
+function rowMajor(mat) {
+  const out = new Float64Array(16);
+  for (let i = 0; i < 4; i++) for (let j = 0; j < 4; j++) out[i * 4 + j] = mat.elements[i][j];
+  return out;
+}
+
+class Renderer {
+  constructor(target = {}, options = {}) {
+    const isCanvas = target && typeof target.getContext === 'function';
+    const opts = isCanvas ? options : Object.assign({}, target, options);
+    this.canvas = isCanvas ? target : null;
+    this.width = opts.width || (this.canvas && this.canvas.width) || 512;    // webgl.js:24 (512 x 512)
+    this.height = opts.height || (this.canvas && this.canvas.height) || 512;
+    this.device = opts.device === undefined ? -1 : opts.device;
+    this.maxBounces = opts.maxBounces || MAXBOUNCES;
+    this.deterministic = !!opts.deterministic;  // frozen schedule (SURVEY §8(d)) instead of Math.random + clock
+    this.accumulation = opts.accumulation || 'mix';
+    this.aov = opts.aov !== false;
+    this.display = opts.display === undefined ? !!this.canvas : !!opts.display;
+    this.lib = native.load();
+    this.ctx = this.lib.create(this.width, this.height, this.device, (this.aov ? 1 : 0) | 2);
+    this.lib.setAccumMode(this.ctx, ACCUM[this.accumulation]);
+    this.timeStart = Date.now();
+    this.filter = filterConfig({ name: 'color', params: {} });
+    this.pixels = null;
+    this.n = 0;
+  }
+
+  update(scene) {
+    this.filter = filterConfig(scene.rendererConfig().filter);
+    const s = scene.serialize();
+    this.lib.setScene(this.ctx, s.objects, s.n, s.texparams, s.tn, s.lights, s.ln, masksOf(scene.tracerConfig()));
+    this.n = s.n;
+    scene.sampleCount = 0;
+  }
+
+  updateObjects(scene) {
+    this.lib.updateObjects(this.ctx, scene.serializeObjects(), this.n);
+  }
+
+  _mvp(scene) { return rowMajor(scene.mat); }
+
+  render(scene) {
+    if (scene.moving) {
+      scene.sampleCount = 0;
+      this.updateObjects(scene);
+    }
+    if (scene.sampleCount === 0) this.lib.reset(this.ctx);  // textureWeight 0: the frame restarts
+    const k = scene.sampleCount++;
+    const mvp = this._mvp(scene);
+    const eye = Float32Array.from(scene.eye.elements);
+    let inv, seed;
+    if (this.deterministic) {
+      const sch = this.lib.schedule(mvp, this.width, this.height, k, 1);
+      inv = sch.inv; seed = sch.seeds[0];
+    } else {
+      inv = this.lib.jitterInverse(mvp, Math.random() * 2 - 1, Math.random() * 2 - 1, this.width, this.height);
+      seed = (Date.now() - this.timeStart) * 0.001;
+    }
+    this.lib.render(this.ctx, inv, eye, seed, this.maxBounces);
+    if (this.display) this.present();
+  }
+
+  // many samples in one launch sequence, deterministic schedule k0 .. k0+spp-1
+  renderSamples(scene, spp) {
+    if (scene.moving) { scene.sampleCount = 0; this.updateObjects(scene); }
+    if (scene.sampleCount === 0) this.lib.reset(this.ctx);
+    const sch = this.lib.schedule(this._mvp(scene), this.width, this.height, scene.sampleCount, spp);
+    this.lib.renderSchedule(this.ctx, sch.inv, sch.seeds, Float32Array.from(scene.eye.elements), this.maxBounces);
+    scene.sampleCount += spp;
+    if (this.display) this.present();
+  }
+
+  // the display pass: pixelFilter over the accumulated frame -> RGBA8 (row 0 = bottom, GL order)
+  image() {
+    const f = this.filter;
+    if (f.aov) {
+      const rb = this.lib.readback(this.ctx, true);
+      const src = f.aov === 'normal' ? rb.normal : rb.position;
+      const out = new Uint8Array(src.length);
+      for (let i = 0; i < src.length; i++) out[i] = Math.floor(Math.min(Math.max(src[i], 0), 1) * 255 + 0.5);
+      return out;
+    }
+    return this.lib.filter(this.ctx, f.kind, f.weights, f.rx, f.ry, f.gamma).rgba8;
+  }
+
+  present() {
+    this.pixels = this.image();
+    if (this.canvas) {
+      const g = this.canvas.getContext('2d');
+      if (g && typeof g.createImageData === 'function') {
+        const img = g.createImageData(this.width, this.height);
+        const rowBytes = this.width * 4;
+        for (let y = 0; y < this.height; y++) {  // GL rows are bottom-up, canvas rows top-down
+          img.data.set(this.pixels.subarray((this.height - 1 - y) * rowBytes, (this.height - y) * rowBytes), y * rowBytes);
+        }
+        g.putImageData(img, 0, 0);
+      }
+    }
+    return this.pixels;
+  }
+
+  readPixels() { return this.lib.readback(this.ctx, false).rgba; }
+  readAccum() { return this.lib.readAccum(this.ctx); }
+  readAOV() { const r = this.lib.readback(this.ctx, true); return { normal: r.normal, position: r.position }; }
+  stats() { return this.lib.stats(this.ctx); }
+  destroy() { if (this.ctx) { this.lib.destroy(this.ctx); this.ctx = null; } }
+}
+
+module.exports = { Renderer, masksOf, MAXBOUNCES };

@@ -1,0 +1,98 @@
+"""The JavaScript host (sail_amd/js: Sail.Scene / Camera / scene.add / Renderer over N-API).
+
+CPU: the JS API serialises every frozen scene to rows, plugin sets, P*MV and filter tables bit-identical
+to what the reference's own Tracer.update / RenderShader produce (tests/golden/fixtures.json).
+GPU: Sail.Renderer -> addon -> libsail_hip.so renders bit-identical to the CPU oracle."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from sail_amd import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+
+@pytest.fixture(scope="module")
+def exported():
+    out = subprocess.run([NODE, os.path.join(ROOT, "sail_amd", "js", "tools", "export_scenes.js")],
+                         capture_output=True, text=True, check=True).stdout
+    return json.loads(out)
+
+
+def bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.uint32)
+
+
+@pytest.mark.parametrize("name", ["C1", "C1g", "C3", "C4", "UI", "ALL"])
+def test_scene_rows_match_reference_serializer(fixtures, exported, name):
+    mine, ref = exported[name], fixtures["scenes"][name]
+    for k in ("n", "tn", "ln", "plugins", "eye"):
+        assert mine[k] == ref[k], k
+    for k in ("objects", "texparams", "lights"):
+        assert np.array_equal(bits(mine[k]), bits(ref[k])), k
+    assert np.array_equal(np.array(mine["mvp_rowmajor"]), np.array(ref["mvp_rowmajor"]))
+    assert mine["filter"]["name"] == ref["filter"]["name"]
+    if "weight_text" in ref["filter"]:
+        assert mine["filter"]["weights64"] == [float(x) for x in ref["filter"]["weight_text"]]
+
+
+def test_committed_frozen_scenes_are_current(exported):
+    with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
+        assert json.load(f) == exported
+
+
+def test_filter_tables_match_reference_codegen(fixtures):
+    spec = {k: v["params"] for k, v in fixtures["filters"].items()}
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "filter_tables.js"), json.dumps(spec)],
+                         capture_output=True, text=True, check=True).stdout
+    mine = json.loads(out)
+    for name, ref in fixtures["filters"].items():
+        assert mine[name]["weights64"] == [float(x) for x in ref["weight_text"]], name
+        # FILTER_WINDOW_RADIUS is the raw text; its numbers are the GLSL radius
+        assert ref["radius_text"] == ref["params"]["r"]
+
+
+def test_js_api_surface():
+    keys = subprocess.run([NODE, "-e", "console.log(Object.keys(require('./sail_amd/js')).sort().join(' '))"],
+                          cwd=ROOT, capture_output=True, text=True, check=True).stdout.split()
+    want = sorted("Renderer Scene Cube Sphere Rectangle Cone Cylinder Disk Hyperboloid Paraboloid AreaLight PointLight "
+                  "SpotLight Cornellbox Camera Control Matte Mirror Metal Glass UniformColor Checkerboard Checkerboard2 "
+                  "Bilerp Mix Scale UV Color Matrix Vector".split())
+    assert keys == want  # index.js:15-46
+
+
+def test_renderer_fails_loudly_without_device():
+    if capi.device_count() > 0:
+        pytest.skip("device present")
+    r = subprocess.run([NODE, "-e", "const S=require('./sail_amd/js'); new S.Renderer({width:8,height:8})"],
+                       cwd=ROOT, capture_output=True, text=True)
+    assert r.returncode != 0 and ("no HIP device" in r.stderr or "not built" in r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,W,H,spp,B,mode,api", [
+    ("C1", 40, 30, 4, 5, "sum", "samples"),
+    ("C3", 32, 32, 3, 5, "mix", "frames"),
+    ("UI", 24, 24, 2, 5, "mix", "samples"),
+])
+def test_js_renderer_bit_exact_vs_oracle(tmp_path, fixtures, exported, name, W, H, spp, B, mode, api):
+    if capi.device_count() < 1:
+        pytest.skip("no HIP device")
+    prefix = str(tmp_path / name)
+    subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "render_check.js"), name, str(W), str(H), str(spp), str(B),
+                    mode, api, prefix], cwd=ROOT, check=True, timeout=300)
+    got = np.fromfile(prefix + ".accum.f32", dtype=np.float32).reshape(H, W, 4)
+    sc = exported[name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    acc_mode = oracle.ACC_SUM if mode == "sum" else oracle.ACC_MIX
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B, accum_mode=acc_mode)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    rgba8 = np.fromfile(prefix + ".rgba8", dtype=np.uint8).reshape(H, W, 4)
+    assert rgba8[..., 3].min() == 255
