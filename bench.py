@@ -77,6 +77,19 @@ def ops_per_segment(sc, masks, mvp, W, H, B):
     return ops / max(segs, 1)
 
 
+def profiled_traffic(px, spp, bounces):
+    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same launch shape
+    (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary.json); None if none matches."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        L = rec.get("launch", {})
+        if L.get("pixels") == px and L.get("spp") == spp and L.get("bounces") == bounces:
+            return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,6 +175,7 @@ def main():
         ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
+        traffic, traffic_src = profiled_traffic(tiles_px, args.launch_spp, B)
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box",
             "value": round(value, 3),
@@ -179,7 +193,7 @@ def main():
                        "launch_spp": args.launch_spp, "partition": f"tiles64x{world}", "segments_per_step": W * H * spp * B},
             "roofline": {
                 "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "ops_per_segment": round(ops_seg, 2), "kernel": "sail_trace_kernel",
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 PMC passes of tools/pmc.sh (gpurun_out/pmc/*) for the trace kernel into one JSON.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports
+half of the bytes of a wide (16 B/lane) coalesced streaming read, which is this kernel's accumulator read,
+so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.
+Usage: tools/pmc_summary.py gpurun_out/pmc out.json [launch_pixels launch_spp bounces]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def load(pdir, name):
+    path = os.path.join(pdir, name, "run_counter_collection.csv")
+    agg = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "sail_trace_kernel" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main():
+    pdir, out = sys.argv[1], sys.argv[2]
+    px = int(sys.argv[3]) if len(sys.argv) > 3 else 1920 * 1080
+    spp = int(sys.argv[4]) if len(sys.argv) > 4 else 32
+    bounces = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+    c = {}
+    for p in ("fetch", "write", "sq", "sq2"):
+        if os.path.isdir(os.path.join(pdir, p)):
+            c.update(load(pdir, p)[0])
+    fetch_b = c["FETCH_SIZE"] * 1024 * 2
+    write_b = c["WRITE_SIZE"] * 1024
+    alg = px * 32
+    waves = c.get("SQ_WAVES", 0)
+    segs = px * spp * bounces
+    rec = {
+        "kernel": "sail_trace_kernel", "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
+        "hbm": {"fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
+                "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,
+                "raw_FETCH_SIZE_KiB": c["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": c["WRITE_SIZE"]},
+        "sq": {k: v for k, v in c.items() if k.startswith("SQ_") or k.startswith("GRBM")},
+    }
+    if waves and "SQ_INSTS_VALU" in c:
+        rec["derived"] = {
+            "valu_insts_per_wave": c["SQ_INSTS_VALU"] / waves,
+            "valu_insts_per_segment_lane": c["SQ_INSTS_VALU"] * 64 / segs,
+            "salu_insts_per_wave": c.get("SQ_INSTS_SALU", 0) / waves,
+        }
+        if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+            # lanes doing work per VALU cycle; 1.0 = no divergence or masked lanes
+            rec["derived"]["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64)
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
