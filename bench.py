@@ -98,13 +98,16 @@ def main():
     ap.add_argument("--spp", type=int, default=CONFIG["spp"])
     ap.add_argument("--launch-spp", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="exercise the torch.distributed + RCCL reduce path even with one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    use_comm = world > 1 or args.force_comm
+    if use_comm:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
@@ -121,7 +124,7 @@ def main():
     ctx = capi.Context(W, H, device=local_rank)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
-    if world > 1:
+    if use_comm:
         ctx.set_partition(rank, world, capi.PART_TILES)
         uid = [capi.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -130,7 +133,7 @@ def main():
     def step():
         ctx.reset()
         ctx.render_schedule(inv, seeds, sc["eye"], B)
-        if world > 1:
+        if use_comm:
             ctx.reduce(0)
 
     def barrier_sync():

@@ -1,10 +1,10 @@
 // oracle/ref_math.h — TEST INFRASTRUCTURE (CPU oracle only; never linked into the product).
 //
-// Bit-defined fp32 transcendentals ("compat" math spec, SURVEY §7 hard parts: RNG parity).
+// Bit-defined fp32 transcendentals ("compat" math spec v2, SURVEY §7 hard parts: RNG parity).
 // GLSL leaves sin/cos/atan/acos/pow precision to the vendor (random.glsl:1-18 evaluates sin at
 // arguments of 1e4..1e6, where a 1-ulp difference yields an unrelated sample), so the build DEFINES
-// each one as: promote the f32 argument to f64, evaluate a fixed sequence of IEEE-754 f64 basic
-// operations (+ - * / only; no FMA contraction, no libm), round the result to f32 once.
+// each one as a fixed sequence of IEEE-754 operations: f64 range reduction for sin/cos/tan, then f32
+// polynomials with explicit fused multiply-adds (fmaf); no contraction anywhere else, no libm.
 // The HIP kernel implements the same spec independently in sail_amd/csrc/sail_math.h; the GPU parity
 // tests check the two bit-for-bit over millions of arguments.
 //
@@ -21,39 +21,13 @@ namespace refm {
 
 static inline double dfloor(double x) { return floor(x); }  // exact on every platform
 
-// ---- sin / cos: Cody-Waite 3-part pi/2 reduction (each part 33 significant bits, so k*Pi is exact
-//      for |k| < 2^20, i.e. |x| < ~1.6e6) followed by Taylor polynomials on [-pi/4, pi/4].
+// ---- sin / cos / tan range reduction: Cody-Waite 3-part pi/2 in f64 (each part 33 significant bits, so
+//      k*P_i is exact for |k| < 2^20, i.e. |x| < ~1.6e6).
 static const double kTwoOverPi = 0.6366197723675814;
 static const double kP1 = 1.5707963267341256;
 static const double kP2 = 6.077100506303966e-11;
 static const double kP3 = 2.0222662487959506e-21;
 
-static inline double sin_poly(double r) {  // r - r^3/3! + ... - r^19/19!
-  const double r2 = r * r;
-  double p = -8.22063524662433e-18;
-  p = p * r2 + 2.8114572543455206e-15;
-  p = p * r2 + -7.647163731819816e-13;
-  p = p * r2 + 1.6059043836821613e-10;
-  p = p * r2 + -2.505210838544172e-08;
-  p = p * r2 + 2.7557319223985893e-06;
-  p = p * r2 + -0.0001984126984126984;
-  p = p * r2 + 0.008333333333333333;
-  p = p * r2 + -0.16666666666666666;
-  return r + (r * r2) * p;
-}
-static inline double cos_poly(double r) {  // 1 - r^2/2! + ... - r^18/18!
-  const double r2 = r * r;
-  double p = -1.5619206968586225e-16;
-  p = p * r2 + 4.779477332387385e-14;
-  p = p * r2 + -1.1470745597729725e-11;
-  p = p * r2 + 2.08767569878681e-09;
-  p = p * r2 + -2.755731922398589e-07;
-  p = p * r2 + 2.48015873015873e-05;
-  p = p * r2 + -0.001388888888888889;
-  p = p * r2 + 0.041666666666666664;
-  p = p * r2 + -0.5;
-  return 1.0 + r2 * p;
-}
 // returns quadrant q (0..3) and reduced r
 static inline double reduce_pio2(double x, int* q) {
   if (!(fabs(x) < 1e15)) { *q = 0; return NAN; }          // inf / NaN / absurd range
@@ -65,77 +39,6 @@ static inline double reduce_pio2(double x, int* q) {
   *q = (int)(ki & 3);
   return r;
 }
-static inline double sin_d(double x) {
-  int q; const double r = reduce_pio2(x, &q);
-  switch (q) {
-    case 0: return sin_poly(r);
-    case 1: return cos_poly(r);
-    case 2: return -sin_poly(r);
-    default: return -cos_poly(r);
-  }
-}
-static inline double cos_d(double x) {
-  int q; const double r = reduce_pio2(x, &q);
-  switch (q) {
-    case 0: return cos_poly(r);
-    case 1: return -sin_poly(r);
-    case 2: return -cos_poly(r);
-    default: return sin_poly(r);
-  }
-}
-
-// ---- atan / atan2: |a| in [0,1] reduced twice (pi/4 then pi/8 shifts) to |z| <= tan(pi/16),
-//      then the odd Taylor series to z^23.
-static const double kPi = 3.141592653589793;
-static const double kPiO2 = 1.5707963267948966;
-static const double kPiO4 = 0.7853981633974483;
-static const double kPiO8 = 0.39269908169872414;
-static const double kTanPiO8 = 0.41421356237309503;
-static const double kTanPiO16 = 0.198912367379658;
-
-static inline double atan_series(double z) {
-  const double z2 = z * z;
-  double p = 1.0 / 23.0;
-  p = -p * z2 + 1.0 / 21.0;
-  p = -p * z2 + 1.0 / 19.0;
-  p = -p * z2 + 1.0 / 17.0;
-  p = -p * z2 + 1.0 / 15.0;
-  p = -p * z2 + 1.0 / 13.0;
-  p = -p * z2 + 1.0 / 11.0;
-  p = -p * z2 + 1.0 / 9.0;
-  p = -p * z2 + 1.0 / 7.0;
-  p = -p * z2 + 1.0 / 5.0;
-  p = -p * z2 + 1.0 / 3.0;
-  p = -p * z2 + 1.0;
-  return z * p;
-}
-// atan for a in [0, 1]
-static inline double atan01(double a) {
-  double off = 0.0;
-  if (a > kTanPiO8) { a = (a - 1.0) / (a + 1.0); off = kPiO4; }     // a in (-0.4143, 0]
-  if (a > kTanPiO16) { a = (a - kTanPiO8) / (1.0 + a * kTanPiO8); off = off + kPiO8; }
-  else if (a < -kTanPiO16) { a = (a + kTanPiO8) / (1.0 - a * kTanPiO8); off = off - kPiO8; }
-  return off + atan_series(a);
-}
-static inline double atan2_d(double y, double x) {
-  if (y != y || x != x) return y + x;                       // NaN
-  if (y == 0.0 && x == 0.0) return 0.0;                    // GLSL: undefined; defined 0
-  const double ay = fabs(y), ax = fabs(x);
-  double r;
-  if (ay <= ax) r = atan01(ay / ax);                        // |angle| <= pi/4
-  else r = kPiO2 - atan01(ax / ay);
-  if (x < 0.0) r = kPi - r;
-  return (y < 0.0) ? -r : r;
-}
-
-// ---- f64 sqrt from a correctly rounded f32 seed plus one Newton step (basic ops only)
-static inline double sqrt_d(double v) {
-  if (!(v > 0.0)) return (v == 0.0) ? 0.0 : NAN;
-  const double s0 = (double)sqrtf((float)v);
-  if (s0 == 0.0) return 0.0;
-  return s0 + (v - s0 * s0) / (2.0 * s0);
-}
-
 // ---- exp2 / log2 in f64 (gamma filter pow only)
 static inline double ldexp_i(double m, int e) {  // m * 2^e by repeated exact scaling
   while (e > 0) { const int s = e > 60 ? 60 : e; m = m * (double)(1ull << s); e -= s; }
@@ -191,22 +94,78 @@ static inline double log_d(double x) {
   return ((double)e * kLn2Hi + (2.0 * s) * p) + (double)e * kLn2Lo;
 }
 
-// ---- the f32 spec functions
-static inline float sin_s(float x) { return (float)sin_d((double)x); }
-static inline float cos_s(float x) { return (float)cos_d((double)x); }
+// ---- the f32 spec functions (spec v2) ------------------------------------------------------------------
+// sin/cos/tan: the f64 Cody-Waite reduction above (exact k*P_i for |x| < ~1.6e6, which covers the hash
+// RNG's 1e4..1e6 arguments), then ONE rounding of r to f32 and f32 polynomials evaluated with fused
+// multiply-adds (fmaf: correctly rounded on every platform). atan/atan2/acos are f32 throughout.
+// Coefficients: least-squares fits made for this build (tools/fit_spec_math.py); accuracy <= 2 ulp.
+static const float kS0 = -0.166666641831398f, kS1 = 0.008332744240760803f, kS2 = -0.0001958730281330645f;
+static const float kC0 = 0.0416666641831398f, kC1 = -0.0013888344401493669f, kC2 = 2.455315006955061e-05f;
+static const float kA[9] = {-0.3333333134651184f, 0.19999729096889496f, -0.142783522605896f, 0.11032091081142426f,
+                            -0.08650501817464828f, 0.062368933111429214f, -0.03571782633662224f,
+                            0.01341481227427721f, -0.002364102052524686f};
+static const float kB[5] = {0.16666673123836517f, 0.07498858869075775f, 0.045000601559877396f,
+                            0.026559552177786827f, 0.03807495906949043f};
+static const float kPiF = 3.14159274f, kPiO2F = 1.57079637f;
+
+static inline float sinpoly_f(float r) {  // r + r^3 P(r^2), |r| <= pi/4
+  const float z = r * r;
+  const float p = fmaf(fmaf(kS2, z, kS1), z, kS0);
+  return fmaf(r * z, p, r);
+}
+static inline float cospoly_f(float r) {  // 1 - r^2/2 + r^4 Q(r^2)
+  const float z = r * r;
+  const float q = fmaf(fmaf(kC2, z, kC1), z, kC0);
+  return fmaf(z * z, q, fmaf(-0.5f, z, 1.0f));
+}
+static inline void sincos_s(float x, float* so, float* co) {
+  int q; const double r = reduce_pio2((double)x, &q);
+  const float rf = (float)r;
+  const float s = sinpoly_f(rf), c = cospoly_f(rf);
+  switch (q) {
+    case 0: *so = s; *co = c; break;
+    case 1: *so = c; *co = -s; break;
+    case 2: *so = -s; *co = -c; break;
+    default: *so = -c; *co = s; break;
+  }
+}
+static inline float sin_s(float x) { float s, c; sincos_s(x, &s, &c); return s; }
+static inline float cos_s(float x) { float s, c; sincos_s(x, &s, &c); return c; }
 static inline float tan_s(float x) {
   int q; const double r = reduce_pio2((double)x, &q);
-  const double s = sin_poly(r), c = cos_poly(r);
-  return (float)((q & 1) ? (-c / s) : (s / c));
+  const float rf = (float)r;
+  const float s = sinpoly_f(rf), c = cospoly_f(rf);
+  return (q & 1) ? (-c / s) : (s / c);
 }
-static inline float atan2_s(float y, float x) { return (float)atan2_d((double)y, (double)x); }
-static inline float atan_s(float x) { return (float)atan2_d((double)x, 1.0); }
+static inline float atan01_f(float t) {  // atan on [0, 1]: t + t^3 P(t^2)
+  const float z = t * t;
+  float p = kA[8];
+  for (int i = 7; i >= 0; i--) p = fmaf(p, z, kA[i]);
+  return fmaf(t * z, p, t);
+}
+static inline float atan2_s(float y, float x) {
+  if (y != y || x != x) return y + x;
+  if (y == 0.0f && x == 0.0f) return 0.0f;  // GLSL: undefined; defined 0
+  const float ay = fabsf(y), ax = fabsf(x);
+  float r = (ay <= ax) ? atan01_f(ay / ax) : kPiO2F - atan01_f(ax / ay);
+  if (x < 0.0f) r = kPiF - r;
+  return (y < 0.0f) ? -r : r;
+}
+static inline float atan_s(float x) { return atan2_s(x, 1.0f); }
+static inline float asinpoly_f(float x) {  // asin on [-0.5, 0.5]: x + x^3 P(x^2)
+  const float z = x * x;
+  float p = kB[4];
+  for (int i = 3; i >= 0; i--) p = fmaf(p, z, kB[i]);
+  return fmaf(x * z, p, x);
+}
 static inline float acos_s(float x) {
-  const double d = (double)x;
-  if (!(d >= -1.0 && d <= 1.0)) return NAN;
-  return (float)atan2_d(sqrt_d((1.0 - d) * (1.0 + d)), d);
+  if (!(x >= -1.0f && x <= 1.0f)) return NAN;
+  const float ax = fabsf(x);
+  if (ax <= 0.5f) return kPiO2F - asinpoly_f(x);
+  const float a2 = 2.0f * asinpoly_f(sqrtf((1.0f - ax) * 0.5f));
+  return (x > 0.0f) ? a2 : kPiF - a2;
 }
-static inline float pow_s(float x, float y) {
+static inline float pow_s(float x, float y) {  // display gamma only: f64 exp/log
   if (x != x || y != y) return NAN;
   if (y == 0.0f) return 1.0f;
   if (x < 0.0f) return NAN;                                // GLSL: undefined for x < 0

@@ -1,11 +1,11 @@
-// sail_math.h — device implementation of the build's bit-defined f32 math spec ("compat" RNG mode).
+// sail_math.h — device implementation of the build's bit-defined f32 math spec v2 ("compat" RNG mode).
 //
 // GLSL leaves sin/cos/atan/acos/pow accuracy to the vendor, and Sail's hash RNG
 // (src/shader/util/random.glsl:1-18) evaluates sin() at 1e4..1e6 where one ulp decides the sample, so
-// the build defines each transcendental as: f32 argument -> f64, a fixed sequence of IEEE f64 basic
-// operations (no FMA: the library is compiled with -ffp-contract=off), one rounding back to f32.
-// The CPU oracle carries an independent copy of the same spec (oracle/ref_math.h); the GPU tests check
-// the two bit-for-bit. MI355X runs f64 VALU at half the f32 rate, so a spec sin costs ~25 f64 ops.
+// the build defines each transcendental as a fixed IEEE operation sequence: an exact f64 Cody-Waite
+// reduction for sin/cos/tan (the only f64 work: ~8 ops), then f32 polynomials with explicit FMAs
+// (<= 2 ulp). The library is compiled with -ffp-contract=off, so no other FMA is formed. The CPU oracle
+// carries an independent copy of the spec (oracle/ref_math.h); the GPU tests check them bit-for-bit.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,32 +19,6 @@ constexpr double kP1 = 1.5707963267341256;
 constexpr double kP2 = 6.077100506303966e-11;
 constexpr double kP3 = 2.0222662487959506e-21;
 
-SM_D double sin_poly(double r) {
-  const double r2 = r * r;
-  double p = -8.22063524662433e-18;
-  p = p * r2 + 2.8114572543455206e-15;
-  p = p * r2 + -7.647163731819816e-13;
-  p = p * r2 + 1.6059043836821613e-10;
-  p = p * r2 + -2.505210838544172e-08;
-  p = p * r2 + 2.7557319223985893e-06;
-  p = p * r2 + -0.0001984126984126984;
-  p = p * r2 + 0.008333333333333333;
-  p = p * r2 + -0.16666666666666666;
-  return r + (r * r2) * p;
-}
-SM_D double cos_poly(double r) {
-  const double r2 = r * r;
-  double p = -1.5619206968586225e-16;
-  p = p * r2 + 4.779477332387385e-14;
-  p = p * r2 + -1.1470745597729725e-11;
-  p = p * r2 + 2.08767569878681e-09;
-  p = p * r2 + -2.755731922398589e-07;
-  p = p * r2 + 2.48015873015873e-05;
-  p = p * r2 + -0.001388888888888889;
-  p = p * r2 + 0.041666666666666664;
-  p = p * r2 + -0.5;
-  return 1.0 + r2 * p;
-}
 SM_D double reduce_pio2(double x, int& q) {
   if (!(fabs(x) < 1e15)) { q = 0; return __builtin_nan(""); }
   const double k = floor(x * kTwoOverPi + 0.5);
@@ -54,71 +28,6 @@ SM_D double reduce_pio2(double x, int& q) {
   q = (int)((long long)k & 3);
   return r;
 }
-SM_D double sin_d(double x) {
-  int q; const double r = reduce_pio2(x, q);
-  const double s = sin_poly(r), c = cos_poly(r);
-  return q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
-}
-SM_D double cos_d(double x) {
-  int q; const double r = reduce_pio2(x, q);
-  const double s = sin_poly(r), c = cos_poly(r);
-  return q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
-}
-// sin and cos of one argument with one reduction (both results are the spec values)
-SM_D void sincos_d(double x, double& so, double& co) {
-  int q; const double r = reduce_pio2(x, q);
-  const double s = sin_poly(r), c = cos_poly(r);
-  so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
-  co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
-}
-
-constexpr double kPi = 3.141592653589793;
-constexpr double kPiO2 = 1.5707963267948966;
-constexpr double kPiO4 = 0.7853981633974483;
-constexpr double kPiO8 = 0.39269908169872414;
-constexpr double kTanPiO8 = 0.41421356237309503;
-constexpr double kTanPiO16 = 0.198912367379658;
-
-SM_D double atan_series(double z) {
-  const double z2 = z * z;
-  double p = 1.0 / 23.0;
-  p = -p * z2 + 1.0 / 21.0;
-  p = -p * z2 + 1.0 / 19.0;
-  p = -p * z2 + 1.0 / 17.0;
-  p = -p * z2 + 1.0 / 15.0;
-  p = -p * z2 + 1.0 / 13.0;
-  p = -p * z2 + 1.0 / 11.0;
-  p = -p * z2 + 1.0 / 9.0;
-  p = -p * z2 + 1.0 / 7.0;
-  p = -p * z2 + 1.0 / 5.0;
-  p = -p * z2 + 1.0 / 3.0;
-  p = -p * z2 + 1.0;
-  return z * p;
-}
-SM_D double atan01(double a) {
-  double off = 0.0;
-  if (a > kTanPiO8) { a = (a - 1.0) / (a + 1.0); off = kPiO4; }
-  if (a > kTanPiO16) { a = (a - kTanPiO8) / (1.0 + a * kTanPiO8); off = off + kPiO8; }
-  else if (a < -kTanPiO16) { a = (a + kTanPiO8) / (1.0 - a * kTanPiO8); off = off - kPiO8; }
-  return off + atan_series(a);
-}
-SM_D double atan2_d(double y, double x) {
-  if (y != y || x != x) return y + x;
-  if (y == 0.0 && x == 0.0) return 0.0;
-  const double ay = fabs(y), ax = fabs(x);
-  double r;
-  if (ay <= ax) r = atan01(ay / ax);
-  else r = kPiO2 - atan01(ax / ay);
-  if (x < 0.0) r = kPi - r;
-  return (y < 0.0) ? -r : r;
-}
-SM_D double sqrt_d(double v) {
-  if (!(v > 0.0)) return (v == 0.0) ? 0.0 : __builtin_nan("");
-  const double s0 = (double)__builtin_sqrtf((float)v);
-  if (s0 == 0.0) return 0.0;
-  return s0 + (v - s0 * s0) / (2.0 * s0);
-}
-
 constexpr double kLn2Hi = 0.6931471803691238;
 constexpr double kLn2Lo = 1.9082149292705877e-10;
 constexpr double kInvLn2 = 1.4426950408889634;
@@ -173,23 +82,69 @@ SM_D double log_d(double x) {
   return ((double)e * kLn2Hi + (2.0 * s) * p) + (double)e * kLn2Lo;
 }
 
-// ---- f32 spec functions ----
-SM_D float sinf_(float x) { return (float)sin_d((double)x); }
-SM_D float cosf_(float x) { return (float)cos_d((double)x); }
-SM_D void sincosf_(float x, float& s, float& c) {
-  double sd, cd; sincos_d((double)x, sd, cd); s = (float)sd; c = (float)cd;
+// ---- f32 spec functions (spec v2): f64 reduction for sin/cos/tan, then f32 polynomials with explicit
+//      fused multiply-adds (v_fma_f32 is correctly rounded: identical to the oracle's fmaf) ----
+constexpr float kS0 = -0.166666641831398f, kS1 = 0.008332744240760803f, kS2 = -0.0001958730281330645f;
+constexpr float kC0 = 0.0416666641831398f, kC1 = -0.0013888344401493669f, kC2 = 2.455315006955061e-05f;
+constexpr float kA0 = -0.3333333134651184f, kA1 = 0.19999729096889496f, kA2 = -0.142783522605896f,
+                kA3 = 0.11032091081142426f, kA4 = -0.08650501817464828f, kA5 = 0.062368933111429214f,
+                kA6 = -0.03571782633662224f, kA7 = 0.01341481227427721f, kA8 = -0.002364102052524686f;
+constexpr float kB0 = 0.16666673123836517f, kB1 = 0.07498858869075775f, kB2 = 0.045000601559877396f,
+                kB3 = 0.026559552177786827f, kB4 = 0.03807495906949043f;
+constexpr float kPiF = 3.14159274f, kPiO2F = 1.57079637f;
+
+SM_D float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+SM_D float sinpoly_f(float r) {
+  const float z = r * r;
+  return fma_(r * z, fma_(fma_(kS2, z, kS1), z, kS0), r);
 }
+SM_D float cospoly_f(float r) {
+  const float z = r * r;
+  return fma_(z * z, fma_(fma_(kC2, z, kC1), z, kC0), fma_(-0.5f, z, 1.0f));
+}
+SM_D void sincosf_(float x, float& so, float& co) {
+  int q; const double r = reduce_pio2((double)x, q);
+  const float rf = (float)r;
+  const float s = sinpoly_f(rf), c = cospoly_f(rf);
+  so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
+  co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
+}
+SM_D float sinf_(float x) { float s, c; sincosf_(x, s, c); return s; }
+SM_D float cosf_(float x) { float s, c; sincosf_(x, s, c); return c; }
 SM_D float tanf_(float x) {
   int q; const double r = reduce_pio2((double)x, q);
-  const double s = sin_poly(r), c = cos_poly(r);
-  return (float)((q & 1) ? (-c / s) : (s / c));
+  const float rf = (float)r;
+  const float s = sinpoly_f(rf), c = cospoly_f(rf);
+  return (q & 1) ? (-c / s) : (s / c);
 }
-SM_D float atan2f_(float y, float x) { return (float)atan2_d((double)y, (double)x); }
-SM_D float atanf_(float x) { return (float)atan2_d((double)x, 1.0); }
+SM_D float atan01_f(float t) {
+  const float z = t * t;
+  float p = kA8;
+  p = fma_(p, z, kA7); p = fma_(p, z, kA6); p = fma_(p, z, kA5); p = fma_(p, z, kA4);
+  p = fma_(p, z, kA3); p = fma_(p, z, kA2); p = fma_(p, z, kA1); p = fma_(p, z, kA0);
+  return fma_(t * z, p, t);
+}
+SM_D float atan2f_(float y, float x) {
+  if (y != y || x != x) return y + x;
+  if (y == 0.0f && x == 0.0f) return 0.0f;
+  const float ay = fabsf(y), ax = fabsf(x);
+  float r = (ay <= ax) ? atan01_f(ay / ax) : kPiO2F - atan01_f(ax / ay);
+  if (x < 0.0f) r = kPiF - r;
+  return (y < 0.0f) ? -r : r;
+}
+SM_D float atanf_(float x) { return atan2f_(x, 1.0f); }
+SM_D float asinpoly_f(float x) {
+  const float z = x * x;
+  float p = kB4;
+  p = fma_(p, z, kB3); p = fma_(p, z, kB2); p = fma_(p, z, kB1); p = fma_(p, z, kB0);
+  return fma_(x * z, p, x);
+}
 SM_D float acosf_(float x) {
-  const double d = (double)x;
-  if (!(d >= -1.0 && d <= 1.0)) return __builtin_nanf("");
-  return (float)atan2_d(sqrt_d((1.0 - d) * (1.0 + d)), d);
+  if (!(x >= -1.0f && x <= 1.0f)) return __builtin_nanf("");
+  const float ax = fabsf(x);
+  if (ax <= 0.5f) return kPiO2F - asinpoly_f(x);
+  const float a2 = 2.0f * asinpoly_f(__builtin_sqrtf((1.0f - ax) * 0.5f));
+  return (x > 0.0f) ? a2 : kPiF - a2;
 }
 SM_D float powf_(float x, float y) {
   if (x != x || y != y) return __builtin_nanf("");

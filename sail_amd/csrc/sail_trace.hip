@@ -90,7 +90,21 @@ D bool quadratic(float A, float B, float C, float& t0, float& t1) {  // utility.
   return true;
 }
 
-struct Ray { V3 o, d; };
+// A ray carries the f64 reciprocals of its direction: every slab test divides by the same three
+// components, and a/b == RN_f32(RN_f64(a * RN_f64(1/b))) for all f32 a, b except results that are
+// nonzero subnormals (the f64 product is within 2^-52 of a/b, while a/b of two floats is never within
+// 2^-49 of an f32 rounding midpoint it does not equal) -- those take the IEEE f32 divide (xdiv).
+struct Ray { V3 o, d; double rx, ry, rz; };
+D Ray mkRay(V3 o, V3 d) {
+  Ray r; r.o = o; r.d = d;
+  r.rx = 1.0 / (double)d.x; r.ry = 1.0 / (double)d.y; r.rz = 1.0 / (double)d.z;
+  return r;
+}
+D float xdiv(float a, float b, double rb) {
+  const float q = (float)((double)a * rb);
+  if (__builtin_expect(fabsf(q) < 0x1p-126f && q != 0.0f, 0)) return a / b;
+  return q;
+}
 struct Hit {
   float d; V3 hit, normal, dpdu, dpdv; bool into; int matRow; V3 sc, emission; int matCategory;
 };
@@ -140,6 +154,8 @@ D V2 concentricSampleDisk(V2 u) {
 }
 
 // ---- textures (shader.texture.js:22-29) ----------------------------------------------------------------
+// UNIFORM_COLOR ignores uv, so hit records skip the UV arithmetic (atan2/acos/divides) for it
+D bool needsUV(const Ctx& c, int texRow) { return to_int(TP(c, texRow, 0)) != SAIL_TEX_UNIFORM; }
 D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
   const int cat = to_int(TP(c, texRow, 0));
   if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
@@ -175,7 +191,9 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
 // ---- slab boxes: cube.glsl:65-87, cornellbox.glsl:67-90, boundbox.glsl:6-17 ------------------------------
 struct Slab { float tNear, tFar; };
 D Slab slab(V3 bmin, V3 bmax, const Ray& r) {
-  const V3 tMin = (bmin - r.o) / r.d, tMax = (bmax - r.o) / r.d;
+  const V3 a0 = bmin - r.o, a1 = bmax - r.o;
+  const V3 tMin = v3(xdiv(a0.x, r.d.x, r.rx), xdiv(a0.y, r.d.y, r.ry), xdiv(a0.z, r.d.z, r.rz));
+  const V3 tMax = v3(xdiv(a1.x, r.d.x, r.rx), xdiv(a1.y, r.d.y, r.ry), xdiv(a1.z, r.d.z, r.rz));
   const V3 t1 = vmin(tMin, tMax), t2 = vmax(tMin, tMax);
   Slab s;
   s.tNear = fmax_(fmax_(t1.x, t1.y), t1.z);
@@ -229,12 +247,14 @@ D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
   h.hit = r.o + t * r.d;
   h.normal = normalForCube(r.o + t * r.d, p);
   dpdBox(h.normal, h.dpdu, h.dpdv);
-  const V3 mn = P3(p, 0), mx = P3(p, 3);
-  const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
-  V2 uv;
-  if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(hh.y / tr.y, hh.z / tr.z);
-  else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(hh.x / tr.x, hh.z / tr.z);
-  else uv = v2(hh.x / tr.x, hh.y / tr.y);
+  V2 uv = v2(0.0f, 0.0f);
+  if (needsUV(c, p.texRow)) {
+    const V3 mn = P3(p, 0), mx = P3(p, 3);
+    const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
+    if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(hh.y / tr.y, hh.z / tr.z);
+    else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(hh.x / tr.x, hh.z / tr.z);
+    else uv = v2(hh.x / tr.x, hh.y / tr.y);
+  }
   h.sc = getSurfaceColor(c, uv, p.texRow);
 }
 D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
@@ -276,22 +296,23 @@ D void sphereHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   V3 hl;
   const float t = sphereT(p, r, &hl);
   const float rad = p.a[3];
-  V3 hit = hl;
-  if (hit.x == 0.0f && hit.y == 0.0f) hit.x = 1e-5f * rad;
-  const float phi = phiOf(hit.y, hit.x);
-  const float u = phi / (2.0f * kPI);
-  const float theta = acosf_(clamp_(hit.z / rad, -1.0f, 1.0f));
-  const float v = theta / kPI;
   (void)t;
-  // computeDpDForSphere (:33-43) on the recomputed (un-guarded) local hit
-  const float th2 = acosf_(clamp_(hl.z / rad, -1.0f, 1.0f));
+  // theta of the UV and of computeDpDForSphere (:33-43) are the same value: the pole guard touches x only
+  const float theta = acosf_(clamp_(hl.z / rad, -1.0f, 1.0f));
+  V2 uv = v2(0.0f, 0.0f);
+  if (needsUV(c, p.texRow)) {
+    V3 hit = hl;
+    if (hit.x == 0.0f && hit.y == 0.0f) hit.x = 1e-5f * rad;
+    uv = v2(phiOf(hit.y, hit.x) / (2.0f * kPI), theta / kPI);
+  }
+  const float th2 = theta;
   const float zRadius = sqrtf_(hl.x * hl.x + hl.y * hl.y);
   const float invZRadius = 1.0f / zRadius;
   const float cosPhi = hl.x * invZRadius, sinPhi = hl.y * invZRadius;
   const V3 dpdu = dpduRot(hl);
   const V3 dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(th2));
   const V3 nl = normalize(cross(dpdv, dpdu));
-  h.sc = getSurfaceColor(c, v2(u, v), p.texRow);
+  h.sc = getSurfaceColor(c, uv, p.texRow);
   h.hit = L2W(hl) + P3(p, 0);
   h.normal = L2W(nl);
   h.dpdu = L2W(dpdu);
@@ -329,7 +350,7 @@ D void rectHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   rectT(p, r, &hl);
   const RectFrame f = rectFrame(p);
   h.dpdu = f.dpdu; h.dpdv = f.dpdv; h.normal = f.normal;
-  h.sc = getSurfaceColor(c, v2(hl.x / f.maxX, hl.y / f.maxY), p.texRow);
+  h.sc = getSurfaceColor(c, needsUV(c, p.texRow) ? v2(hl.x / f.maxX, hl.y / f.maxY) : v2(0.0f, 0.0f), p.texRow);
   h.hit = localToWorld(hl, f.normal, f.ss, f.ts) + P3(p, 0);
 }
 
@@ -444,16 +465,16 @@ D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dp
 D void coneHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   V3 hit; coneT(p, r, &hit);
   const float hh = p.a[3];
-  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = hit.z / hh;
+  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
   const float vv = hit.z / hh;
   const V3 dpdv = v3(-hit.x / (1.0f - vv), -hit.y / (1.0f - vv), hh);
-  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), dpdv, h);
+  finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
 D void cylinderHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   V3 hit; cylinderT(p, r, &hit);
   const float hh = p.a[3];
-  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = hit.z / hh;
-  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), v3(0.0f, 0.0f, hh), h);
+  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
+  finishLocal(c, p, hit, uv, dpduRot(hit), v3(0.0f, 0.0f, hh), h);
 }
 D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperboloid.glsl:41-46
   float sinPhi, cosPhi; sincosf_(phi, sinPhi, cosPhi);
@@ -478,21 +499,23 @@ D void paraDpD(V3 hit, float zMax, float zMin, V3& dpdu, V3& dpdv) {  // parabol
 D void paraHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   V3 hit; paraT(p, r, &hit);
   const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
-  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI), v = (hit.z - zMin) / (zMax - zMin);
+  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), (hit.z - zMin) / (zMax - zMin)) : v2(0.0f, 0.0f);
   V3 dpdu, dpdv;
   paraDpD(hit, zMax, zMin, dpdu, dpdv);
-  finishLocal(c, p, hit, v2(u, v), dpdu, dpdv, h);
+  finishLocal(c, p, hit, uv, dpdu, dpdv, h);
 }
 D void diskHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   V3 hit; diskT(p, r, &hit);
   const float rad = p.a[3], ri = p.a[4];
   const float dist2 = hit.x * hit.x + hit.y * hit.y;
-  const float u = phiOf(hit.y, hit.x) / (2.0f * kPI);
-  const float rHit = sqrtf_(dist2);
-  const float oneMinusV = ((rHit - ri) / (rad - ri));
-  const float v = 1.0f - oneMinusV;
+  V2 uv = v2(0.0f, 0.0f);
+  if (needsUV(c, p.texRow)) {
+    const float rHit = sqrtf_(dist2);
+    const float oneMinusV = ((rHit - ri) / (rad - ri));
+    uv = v2(phiOf(hit.y, hit.x) / (2.0f * kPI), 1.0f - oneMinusV);
+  }
   const V3 dpdv = v3(hit.x, hit.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
-  finishLocal(c, p, hit, v2(u, v), dpduRot(hit), dpdv, h);
+  finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
 
 D float primT(const SailPrim& p, const Ray& r) {
@@ -853,21 +876,21 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
     const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
     const V3 toLight = p - ins.hit;
     const V3 nt = normalize(toLight);
-    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    const Ray sr = mkRay(ins.hit, toLight);
     if (testShadow(c, sr)) return v3s(0.0f);
     return em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
   } else if (cat == SAIL_POINT) {
     const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
     const V3 p = from + uniformSampleSphere(u2) * 0.1f;
     const V3 toLight = p - ins.hit;
-    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    const Ray sr = mkRay(ins.hit, toLight);
     if (testShadow(c, sr)) return v3s(0.0f);
     return em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
   } else if (cat == SAIL_SPOT) {
     const float ctw = L[1], cfs = L[2];
     const V3 from = v3(L[3], L[4], L[5]), em = v3(L[6], L[7], L[8]);
     const V3 toLight = from - ins.hit;
-    Ray sr; sr.o = ins.hit; sr.d = toLight;
+    const Ray sr = mkRay(ins.hit, toLight);
     if (testShadow(c, sr)) return v3s(0.0f);
     const V3 nt = normalize(toLight);
     const float d = length(toLight);
@@ -895,7 +918,8 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigne
     // shade()
     const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
     const V3 wo = worldToLocal(-ray.d, ins.normal, ss, ts);
-    const V2 u2 = random2(c, seed);
+    // the hash is evaluated only for materials that consume it (matte/metal/glass; mirror is deterministic)
+    const V2 u2 = (ins.matCategory != SAIL_MIRROR) ? random2(c, seed) : v2(0.0f, 0.0f);
     V3 wiL, f;
     const V3 mat = material(c, ins, u2, wo, wiL, f);
     const V3 _fpdf = vclamp01(mat);
@@ -906,8 +930,7 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigne
     e = e + sh * fpdf;
     fpdf = fpdf * _fpdf;
     const float outdot = dot(ins.normal, wi);
-    ray.o = ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f);
-    ray.d = wi;
+    ray = mkRay(ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f), wi);
   }
   return e;
 }
@@ -948,9 +971,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_trace_kernel(SailTraceArg
     const SailSample& S = A.samples[k];
     const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
     const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
-    Ray ray;
-    ray.o = eye;
-    ray.d = tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t));
+    const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     nAov = v3s(0.0f); pAov = v3s(0.0f);
     const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs);
     if (A.accumMode == 0) {
@@ -1066,6 +1087,9 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
     case 6: r = atanf_(x[i]); break;
     case 7: r = sqrtf_(x[i]); break;
     case 8: r = x[i] / y[i]; break;
+    case 9: r = __builtin_fminf(x[i], y[i]); break;   // hardware v_min_f32 (diagnostic)
+    case 10: r = __builtin_fmaxf(x[i], y[i]); break;  // hardware v_max_f32 (diagnostic)
+    case 11: { const double rb = 1.0 / (double)y[i]; r = xdiv(x[i], y[i], rb); break; }  // shared-reciprocal divide
     default: break;
   }
   out[i] = r;
