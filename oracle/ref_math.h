@@ -9,7 +9,8 @@
 // tests check the two bit-for-bit over millions of arguments.
 //
 // Also defined here (GLSL semantics the reference leaves open, SURVEY §7 "undefined behaviour"):
-//   min/max  -> select form that returns the non-NaN operand (GPU v_min/v_max behaviour); ties keep a
+//   min/max  -> IEEE-754-2019 minimumNumber/maximumNumber (NaN -> other operand, -0 < +0), which is what
+//               GLSL min/max compile to on AMD GPUs (v_min_f32 / v_max_f32)
 //   sqrt     -> IEEE correctly-rounded f32 sqrt
 //   int(x)   -> truncation, NaN -> 0, saturating
 #pragma once
@@ -176,8 +177,22 @@ static inline float exp_s(float x) { return (float)exp_d((double)x); }
 static inline float log_s(float x) { return (float)log_d((double)x); }
 
 // GLSL builtins with defined NaN behaviour
-static inline float fmin_s(float a, float b) { return (b < a) ? b : ((a != a) ? b : a); }
-static inline float fmax_s(float a, float b) { return (a < b) ? b : ((a != a) ? b : a); }
+// min/max as the MI355X v_min_f32/v_max_f32 compute them (measured: tools/probe_minmax.py): a NaN operand
+// yields the other operand; -0 orders below +0 whatever the operand order.
+static inline float fmin_s(float a, float b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  if (a < b) return a;
+  if (b < a) return b;
+  return signbit(a) ? a : b;
+}
+static inline float fmax_s(float a, float b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  if (a > b) return a;
+  if (b > a) return b;
+  return signbit(a) ? b : a;
+}
 static inline float floor_s(float x) { return floorf(x); }
 static inline float fract_s(float x) { return x - floorf(x); }
 static inline float sqrt_s(float x) { return sqrtf(x); }

@@ -1396,6 +1396,10 @@ void oracle_math(int fn, const float* x, const float* y, float* out, int count) 
       case 6: out[i] = refm::atan_s(x[i]); break;
       case 7: out[i] = refm::sqrt_s(x[i]); break;
       case 8: out[i] = x[i] / y[i]; break;
+      case 9: out[i] = refm::fmin_s(x[i], y[i]); break;
+      case 10: out[i] = refm::fmax_s(x[i], y[i]); break;
+      case 11: out[i] = x[i] / y[i]; break;
+      case 12: out[i] = refm::fmin_s(refm::fmax_s(x[i], 0.0f), 1.0f); break;
       default: out[i] = 0.0f; break;
     }
   }

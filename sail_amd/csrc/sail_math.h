@@ -153,9 +153,9 @@ SM_D float powf_(float x, float y) {
   if (x == 0.0f) return (y > 0.0f) ? 0.0f : __builtin_inff();
   return (float)exp_d((double)y * log_d((double)x));
 }
-// GLSL min/max/clamp with defined NaN behaviour (return the non-NaN operand; ties keep the first)
-SM_D float fmin_(float a, float b) { return (b < a) ? b : ((a != a) ? b : a); }
-SM_D float fmax_(float a, float b) { return (a < b) ? b : ((a != a) ? b : a); }
+// GLSL min/max/clamp: the hardware v_min_f32/v_max_f32 (a NaN operand yields the other; -0 < +0)
+SM_D float fmin_(float a, float b) { return __builtin_fminf(a, b); }
+SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 SM_D float clamp_(float x, float lo, float hi) { return fmin_(fmax_(x, lo), hi); }
 SM_D float fract_(float x) { return x - floorf(x); }
 SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }

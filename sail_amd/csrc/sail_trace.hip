@@ -1087,9 +1087,10 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
     case 6: r = atanf_(x[i]); break;
     case 7: r = sqrtf_(x[i]); break;
     case 8: r = x[i] / y[i]; break;
-    case 9: r = __builtin_fminf(x[i], y[i]); break;   // hardware v_min_f32 (diagnostic)
-    case 10: r = __builtin_fmaxf(x[i], y[i]); break;  // hardware v_max_f32 (diagnostic)
+    case 9: r = fmin_(x[i], y[i]); break;
+    case 10: r = fmax_(x[i], y[i]); break;
     case 11: { const double rb = 1.0 / (double)y[i]; r = xdiv(x[i], y[i], rb); break; }  // shared-reciprocal divide
+    case 12: r = clamp_(x[i], 0.0f, 1.0f); break;
     default: break;
   }
   out[i] = r;

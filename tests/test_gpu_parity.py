@@ -51,15 +51,24 @@ def _args(fn, rng, n):
         return rng.normal(size=n) * 10 ** rng.uniform(-3, 3, n), None
     if fn == 7:
         return np.abs(rng.normal(size=n)) * 10 ** rng.uniform(-10, 10, n), None
+    if fn in (9, 10, 12):  # min / max / clamp: signed zeros, NaN, inf and ordinary values, every pairing
+        special = np.array([0.0, -0.0, 1.0, -1.0, np.nan, np.inf, -np.inf, 0.5, 2.0, -1e-30], np.float32)
+        xs, ys = np.meshgrid(special, special)
+        x = np.concatenate([xs.ravel(), rng.normal(size=n).astype(np.float32)])
+        y = np.concatenate([ys.ravel(), rng.normal(size=n).astype(np.float32)])
+        return x, y
+    if fn == 11:  # shared-reciprocal divide vs IEEE divide over raw bit patterns (all classes)
+        bits = rng.integers(0, 2 ** 32, (2, n), dtype=np.uint64).astype(np.uint32)
+        return bits[0].view(np.float32), bits[1].view(np.float32)
     return rng.normal(size=n) * 100, rng.normal(size=n) * 10 ** rng.uniform(-5, 5, n)
 
 
-@pytest.mark.parametrize("fn", list(range(9)))
+@pytest.mark.parametrize("fn", list(range(13)))
 def test_math_spec_bit_exact(gpu, fn):
     rng = np.random.default_rng(1000 + fn)
     x, y = _args(fn, rng, 1 << 18)
-    x = x.astype(np.float32)
-    y = (np.zeros_like(x) if y is None else y).astype(np.float32)
+    x = np.asarray(x).astype(np.float32)
+    y = (np.zeros_like(x) if y is None else np.asarray(y)).astype(np.float32)
     got = capi.math_probe(fn, x, y)
     want = oracle.math(fn, x, y)
     same = bit_equal(got, want)
