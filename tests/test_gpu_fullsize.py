@@ -1,0 +1,72 @@
+"""BASELINE.json's full frame sizes on the GPU, checked through properties that do not need a full CPU
+render: oracle-rendered crops of the same frame (bit-exact), finiteness / sample counts, and the 8-rank
+tile split emulated on one device summing to the 1-rank frame bit for bit."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from sail_amd import capi
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def frozen():
+    if capi.device_count() < 1:
+        pytest.skip("no HIP device")
+    with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
+        return json.load(f)
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+
+
+# (config, scene, W, H, bounces, spp) — BASELINE.json configs[1..3]
+FULL = [("C2", "C1", 1920, 1080, 8, 4), ("C3", "C3", 1920, 1080, 8, 2), ("C4", "C4", 3840, 2160, 12, 1)]
+
+
+@pytest.mark.parametrize("cfg,name,W,H,B,spp", FULL)
+def test_full_frame_crops_match_oracle(frozen, cfg, name, W, H, B, spp):
+    sc = frozen[name]
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    ctx = capi.Context(W, H)
+    ctx.set_scene_dict(sc)
+    ctx.render_schedule(inv, seeds, sc["eye"], B)
+    got = ctx.read_accum()
+    ctx.close()
+    assert np.isfinite(got).all()
+    assert (got[..., 3] == spp).all()
+    rng = np.random.default_rng(hash(cfg) % 2 ** 32)
+    masks = capi.plugin_masks(sc["plugins"])
+    c = 8
+    crops = [(0, 0), (W - c, H - c), (W // 2 - c // 2, H // 2 - c // 2)] + \
+            [(int(rng.integers(0, W - c)), int(rng.integers(0, H - c))) for _ in range(5)]
+    for x0, y0 in crops:
+        want = np.zeros((H, W, 4), np.float32)
+        oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=want)
+        assert _bits_equal(got[y0:y0 + c, x0:x0 + c], want[y0:y0 + c, x0:x0 + c]), (cfg, x0, y0)
+
+
+def test_c2_eight_rank_split_equals_single_rank(frozen):
+    sc = frozen["C1"]
+    W, H, B, spp = 1920, 1080, 8, 2
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    total = np.zeros((H, W, 4), np.float32)
+    ctx = capi.Context(W, H)
+    ctx.set_scene_dict(sc)
+    for rank in range(8):
+        ctx.set_partition(rank, 8)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        total += ctx.read_accum()
+    ctx.set_partition(0, 1)
+    ctx.render_schedule(inv, seeds, sc["eye"], B)
+    full = ctx.read_accum()
+    ctx.close()
+    assert _bits_equal(total, full)
