@@ -26,41 +26,51 @@ sys.path.insert(0, ROOT)
 
 from sail_amd import capi  # noqa: E402
 
-# BASELINE.json configs[1]
-CONFIG = {"workload": "cornell_box_readme_C2", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024}
+# BASELINE.json configs: [1] is the headline (default); the others are selectable with --config for study
+CONFIGS = {
+    "C2": {"workload": "cornell_box_readme_C2", "scene": "C1", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
+    "C3": {"workload": "materials_demo_C3", "scene": "C3", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
+    "C4": {"workload": "random64_C4", "scene": "C4", "width": 3840, "height": 2160, "bounces": 12, "spp": 256},
+    "C5": {"workload": "cornell_box_converged_C5", "scene": "C1", "width": 1920, "height": 1080, "bounces": 16, "spp": 65536},
+}
+CONFIG = CONFIGS["C2"]
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 
 
-def load_scene():
-    """The frozen C1/C2 Cornell box rows (captured from the reference's own serializer) + its camera."""
-    path = os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "tests", "golden", "fixtures.json")
-        with open(path) as f:
-            sc = json.load(f)["scenes"]["C1"]
-    else:
-        with open(path) as f:
-            sc = json.load(f)["C1"]
-    return sc
+def load_scene(name="C1"):
+    """Frozen scene rows exported by this build's JS API (sail_amd/scenes/frozen.json; equal to the
+    reference serializer's output, tests/test_js_host.py)."""
+    with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
+        return json.load(f)[name]
 
 
-def cpu_baseline(sc, masks, mvp, W, H, B):
-    """The CPU oracle (single-threaded C++ restatement of the shader) on a bounded centre crop."""
+def cpu_baseline(sc, masks, mvp, W, H, B, budget_s=10.0):
+    """The CPU oracle (single-threaded C++ restatement of the shader) timed on a bounded sample of the same
+    frame: 32x32 crops spiralling out from the centre, 4 spp each, until ~budget_s of CPU work."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle  # test infrastructure: CPU reference, used here only as the timed baseline
-    cw, ch, spp = 192, 108, 12
-    x0, y0 = (W - cw) // 2, (H - ch) // 2
+    import oracle  # test infrastructure: the CPU reference, used here only as the timed baseline
+    spp, c = 8, 32
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
-    oracle.reset_counters()
     acc = np.zeros((H, W, 4), np.float32)
+    cx, cy = (W - c) // 2, (H - c) // 2
+    offsets = sorted(((dx, dy) for dx in range(-6, 7) for dy in range(-6, 7)), key=lambda d: d[0] ** 2 + d[1] ** 2)
+    oracle.reset_counters()
     t0 = time.perf_counter()
-    oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, cw, ch), accum=acc)
+    crops = 0
+    for dx, dy in offsets:
+        x0, y0 = cx + dx * c, cy + dy * c
+        if x0 < 0 or y0 < 0 or x0 + c > W or y0 + c > H:
+            continue
+        oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=acc)
+        crops += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
     dt = time.perf_counter() - t0
-    segs = cw * ch * spp * B
+    segs, _ = oracle.counters()
     return {"value": segs / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sail_oracle.cpp single thread, {cw}x{ch} centre crop of the C2 frame, {spp} spp x {B} "
-                      f"bounces = {segs} nominal segments in {dt:.2f} s"}
+            "sample": f"oracle/sail_oracle.cpp single thread: {crops} centre-out {c}x{c} crops of the frame, {spp} spp x "
+                      f"{B} bounces = {segs} segments (exact count) in {dt:.2f} s"}
 
 
 def ops_per_segment(sc, masks, mvp, W, H, B):
@@ -95,7 +105,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=CONFIG["spp"])
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--launch-spp", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-comm", action="store_true",
@@ -114,11 +125,13 @@ def main():
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = tdist
 
-    W, H, B, spp = CONFIG["width"], CONFIG["height"], CONFIG["bounces"], args.spp
-    sc = load_scene()
+    cfg = CONFIGS[args.config]
+    W, H, B = cfg["width"], cfg["height"], cfg["bounces"]
+    spp = args.spp if args.spp else cfg["spp"]
+    sc = load_scene(cfg["scene"])
     masks = capi.plugin_masks(sc["plugins"])
-    # makePerspective(55, W/H, 1, 100) (camera.js:16) with the frozen README camera
-    mvp = capi.camera(sc["eye"], [2.78, 2.73, 2.79], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    # makePerspective(55, W/H, 1, 100) (camera.js:16) with the scene's frozen camera
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
 
     ctx = capi.Context(W, H, device=local_rank)
@@ -180,7 +193,8 @@ def main():
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
         traffic, traffic_src = profiled_traffic(tiles_px, args.launch_spp, B)
         rec = {
-            "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box",
+            "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
+                      else f"Msamples/s (paths x bounces), {cfg['workload']}",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -192,7 +206,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: frozen README Cornell box rows (reference serializer), deterministic sample schedule",
-            "config": {"workload": CONFIG["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
+            "config": {"workload": cfg["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
                        "launch_spp": args.launch_spp, "partition": f"tiles64x{world}", "segments_per_step": W * H * spp * B},
             "roofline": {
                 "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
