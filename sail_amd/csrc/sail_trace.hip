@@ -27,6 +27,16 @@
 
 using namespace sm;
 
+#ifndef SAIL_FAST_RCP
+#define SAIL_FAST_RCP 1
+#endif
+#ifndef SAIL_XDIV_NORMALIZE
+#define SAIL_XDIV_NORMALIZE 0
+#endif
+#ifndef SAIL_PRIMS_LDS
+#define SAIL_PRIMS_LDS 0
+#endif
+
 #define D __device__ __forceinline__
 
 namespace {
@@ -54,7 +64,17 @@ D V2 operator*(float s, V2 a) { return v2(s * a.x, s * a.y); }
 D float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 D float length(V3 v) { return sqrtf_(dot(v, v)); }
+D float xdiv(float a, float b, double rb);
+D double rcp_exact(float b);
+#if SAIL_XDIV_NORMALIZE
+D V3 normalize(V3 v) {
+  const float len = length(v);
+  const double rl = rcp_exact(len);
+  return v3(xdiv(v.x, len, rl), xdiv(v.y, len, rl), xdiv(v.z, len, rl));
+}
+#else
 D V3 normalize(V3 v) { return v / length(v); }
+#endif
 D V3 vmin(V3 a, V3 b) { return v3(fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)); }
 D V3 vmax(V3 a, V3 b) { return v3(fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)); }
 D V3 vclamp01(V3 x) { return vmin(vmax(x, v3s(0.0f)), v3s(1.0f)); }
@@ -95,9 +115,25 @@ D bool quadratic(float A, float B, float C, float& t0, float& t1) {  // utility.
 // nonzero subnormals (the f64 product is within 2^-52 of a/b, while a/b of two floats is never within
 // 2^-49 of an f32 rounding midpoint it does not equal) -- those take the IEEE f32 divide (xdiv).
 struct Ray { V3 o, d; double rx, ry, rz; };
+// f64 reciprocal of an f32 with relative error <= ~2^-52 (what xdiv needs): an f32 hardware reciprocal
+// refined by two f64 Newton steps; zero/inf/NaN/extreme magnitudes take the IEEE f64 divide.
+D double rcp_exact(float b) {
+#if SAIL_FAST_RCP
+  const float ab = fabsf(b);
+  if (!(ab >= 0x1p-120f && ab <= 0x1p120f)) return 1.0 / (double)b;
+  const double bd = (double)b;
+  double r = (double)__builtin_amdgcn_rcpf(b);
+  double e = __builtin_fma(-bd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-bd, r, 1.0);
+  return __builtin_fma(r, e, r);
+#else
+  return 1.0 / (double)b;
+#endif
+}
 D Ray mkRay(V3 o, V3 d) {
   Ray r; r.o = o; r.d = d;
-  r.rx = 1.0 / (double)d.x; r.ry = 1.0 / (double)d.y; r.rz = 1.0 / (double)d.z;
+  r.rx = rcp_exact(d.x); r.ry = rcp_exact(d.y); r.rz = rcp_exact(d.z);
   return r;
 }
 D float xdiv(float a, float b, double rb) {
@@ -943,7 +979,10 @@ D float q8(float v) {
 }  // namespace
 
 // 256 threads = 16x16 pixel block; wave w covers the 16x4 strip rows 4w..4w+3; 16 blocks per 64x64 tile.
-extern "C" __global__ void __launch_bounds__(256) sail_trace_kernel(SailTraceArgs A) {
+#ifndef SAIL_TRACE_MIN_WAVES
+#define SAIL_TRACE_MIN_WAVES 6
+#endif
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
   const int ownedTile = blockIdx.x >> 4;
   const int sub = blockIdx.x & 15;
   const int tile = A.rank + ownedTile * A.world;
@@ -951,10 +990,26 @@ extern "C" __global__ void __launch_bounds__(256) sail_trace_kernel(SailTraceArg
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int x = tx * 64 + (sub & 3) * 16 + (lane & 15);
   const int y = ty * 64 + (sub >> 2) * 16 + wave * 4 + (lane >> 4);
+#if SAIL_PRIMS_LDS
+  // stage the decoded primitives in LDS once per workgroup; reads are then wave-uniform ds_reads
+  __shared__ SailPrim sPrims[SAIL_PRIMS_LDS];
+  {
+    const float4* src = reinterpret_cast<const float4*>(A.prims);
+    float4* dst = reinterpret_cast<float4*>(sPrims);
+    const int nv = A.n * (int)(sizeof(SailPrim) / sizeof(float4));
+    for (int i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+    __syncthreads();
+  }
+#endif
   if (x >= A.W || y >= A.H || ownedTile >= A.ownedTiles) return;
 
   Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.prims = A.prims;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow;
+#if SAIL_PRIMS_LDS
+  c.prims = sPrims;
+#else
+  c.prims = A.prims;
+#endif
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
@@ -1089,7 +1144,7 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
     case 8: r = x[i] / y[i]; break;
     case 9: r = fmin_(x[i], y[i]); break;
     case 10: r = fmax_(x[i], y[i]); break;
-    case 11: { const double rb = 1.0 / (double)y[i]; r = xdiv(x[i], y[i], rb); break; }  // shared-reciprocal divide
+    case 11: r = xdiv(x[i], y[i], rcp_exact(y[i])); break;  // shared-reciprocal divide
     case 12: r = clamp_(x[i], 0.0f, 1.0f); break;
     default: break;
   }
