@@ -206,6 +206,42 @@ int resetAccum(sail_ctx* c) {
 // Decode the objects rows into SailPrim records with the reference's addressing rules
 // (shader.shape.js:34 row = float(i)/float(n-1); parseX readFloat/readVec3 columns; matIndex/texIndex as
 // readFloat(...)/float(tn-1) normalised rows; cornellbox.glsl:17 material from slot 7).
+// Rectangle frame (rectangle.glsl:32-44), the same f32 operations in the same order as the per-ray GLSL,
+// evaluated once per scene: a[6..8] normal, a[9..11] ss, a[12..14] ts, a[15] maxX, a[16] maxY and
+// a[17] the area-light pdf 1/(|x||y|) of sampleGeometry (shader.shape.js:53-67). Host f32 arithmetic is
+// IEEE (SSE, no contraction), so the values are bit-identical to the kernel's own evaluation.
+struct F3 { float x, y, z; };
+F3 f3cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+float f3dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+F3 f3div(F3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+void rectFrameHost(SailPrim& p) {
+  const F3 dpdu{p.a[3] - p.a[0], 0.0f, 0.0f}, dpdv{0.0f, p.a[4] - p.a[1], p.a[5] - p.a[2]};
+  const F3 cr = f3cross(dpdu, dpdv);
+  const F3 normal = f3div(cr, sqrtf(f3dot(cr, cr)));
+  const float maxX = sqrtf(f3dot(dpdu, dpdu)), maxY = sqrtf(f3dot(dpdv, dpdv));
+  const F3 ss = f3div(dpdu, maxX);
+  const F3 ts = f3cross(normal, ss);
+  const float f[12] = {normal.x, normal.y, normal.z, ss.x, ss.y, ss.z, ts.x, ts.y, ts.z, maxX, maxY,
+                       1.0f / (maxX * maxY)};
+  memcpy(&p.a[6], f, sizeof f);
+}
+
+// GLSL min/max as v_min_f32/v_max_f32 evaluate them (a NaN operand yields the other; -0 < +0)
+float hwmin(float a, float b) { if (a != a) return b; if (b != b) return a; if (a < b) return a; if (b < a) return b; return signbit(a) ? a : b; }
+float hwmax(float a, float b) { if (a != a) return b; if (b != b) return a; if (a > b) return a; if (b > a) return b; return signbit(a) ? b : a; }
+// Per-scene quadric constants, each the exact f32 expression the GLSL evaluates per ray:
+//   cone (cone.glsl:58-59)            a[5] = (rad / h)^2
+//   hyperboloid (hyperboloid.glsl:13-24)  a[11] = max(r1, r2), a[12] = min(p1.z, p2.z), a[13] = max(p1.z, p2.z)
+//   paraboloid (paraboloid.glsl:60)   a[6] = zMax / (rad * rad)
+void quadricHost(SailPrim& p) {
+  if (p.type == SAIL_CONE) { float k = p.a[4] / p.a[3]; p.a[5] = k * k; }
+  if (p.type == SAIL_HYPERBOLOID) {
+    const float r1 = sqrtf(p.a[3] * p.a[3] + p.a[4] * p.a[4]), r2 = sqrtf(p.a[6] * p.a[6] + p.a[7] * p.a[7]);
+    p.a[11] = hwmax(r1, r2); p.a[12] = hwmin(p.a[5], p.a[8]); p.a[13] = hwmax(p.a[5], p.a[8]);
+  }
+  if (p.type == SAIL_PARABOLOID) p.a[6] = hwmax(p.a[3], p.a[4]) / (p.a[5] * p.a[5]);
+}
+
 void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk) {
   TexView o{objects, 18, n};
   const float L = 17.0f;
@@ -226,6 +262,7 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
         p.rev = to_int(o.readFloat(7.0f, rc, L)) == 1;
         p.matRow = row(o.readFloat(8.0f, rc, L)); p.texRow = row(o.readFloat(9.0f, rc, L));
         o.readVec3(10.0f, rc, L, v3);
+        if (cat == SAIL_RECTANGLE) rectFrameHost(p);
         break;
       case SAIL_SPHERE:
         o.readVec3(1.0f, rc, L, &p.a[0]); p.a[3] = o.readFloat(4.0f, rc, L);
@@ -263,6 +300,7 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
       default: break;
     }
     p.em[0] = v3[0]; p.em[1] = v3[1]; p.em[2] = v3[2];
+    quadricHost(p);
     // only slabs return t > EPSILON strictly; anything else may tie or undercut EPSILON, so shadow
     // rays must then find the true closest distance (shader.light.js:24-31)
     if (cat != SAIL_CUBE && cat != SAIL_CORNELLBOX) *anyHitOk = 0;

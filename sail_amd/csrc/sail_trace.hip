@@ -33,6 +33,12 @@ using namespace sm;
 #ifndef SAIL_XDIV_NORMALIZE
 #define SAIL_XDIV_NORMALIZE 0
 #endif
+#ifndef SAIL_SWEEP_HL
+#define SAIL_SWEEP_HL 1
+#endif
+#ifndef SAIL_SS_UNIT
+#define SAIL_SS_UNIT 0
+#endif
 #ifndef SAIL_PRIMS_LDS
 #define SAIL_PRIMS_LDS 0
 #endif
@@ -328,11 +334,8 @@ D float phiOf(float y, float x) {
   return phi;
 }
 D V3 dpduRot(V3 hit) { return v3(-2.0f * kPI * hit.y, 2.0f * kPI * hit.x, 0.0f); }
-D void sphereHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hl;
-  const float t = sphereT(p, r, &hl);
+D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const float rad = p.a[3];
-  (void)t;
   // theta of the UV and of computeDpDForSphere (:33-43) are the same value: the pole guard touches x only
   const float theta = acosf_(clamp_(hl.z / rad, -1.0f, 1.0f));
   V2 uv = v2(0.0f, 0.0f);
@@ -357,16 +360,13 @@ D void sphereHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
 
 // ---- rectangle.glsl:32-63 ---------------------------------------------------------------------------------
 struct RectFrame { V3 dpdu, dpdv, normal, ss, ts; float maxX, maxY; };
-D RectFrame rectFrame(const SailPrim& p) {
+D RectFrame rectFrame(const SailPrim& p) {  // rectangle.glsl:32-44; the divides/roots are per scene (host)
   RectFrame f;
   const V3 mn = P3(p, 0), mx = P3(p, 3);
   f.dpdu = v3(mx.x - mn.x, 0.0f, 0.0f);
   f.dpdv = v3(0.0f, mx.y - mn.y, mx.z - mn.z);
-  f.normal = normalize(cross(f.dpdu, f.dpdv));
-  f.maxX = length(f.dpdu);
-  f.maxY = length(f.dpdv);
-  f.ss = f.dpdu / f.maxX;
-  f.ts = cross(f.normal, f.ss);
+  f.normal = P3(p, 6); f.ss = P3(p, 9); f.ts = P3(p, 12);
+  f.maxX = p.a[15]; f.maxY = p.a[16];
   return f;
 }
 D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
@@ -381,9 +381,7 @@ D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
   if (hitOut) *hitOut = hit;
   return t;
 }
-D void rectHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hl;
-  rectT(p, r, &hl);
+D void rectHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const RectFrame f = rectFrame(p);
   h.dpdu = f.dpdu; h.dpdv = f.dpdv; h.normal = f.normal;
   h.sc = getSurfaceColor(c, needsUV(c, p.texRow) ? v2(hl.x / f.maxX, hl.y / f.maxY) : v2(0.0f, 0.0f), p.texRow);
@@ -411,8 +409,7 @@ D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const float h = p.a[3], rad = p.a[4];
   if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
-  float k = rad / h;
-  k = k * k;
+  const float k = p.a[5];  // (rad / h)^2, per scene
   const float a = d.x * d.x + d.y * d.y - k * d.z * d.z;
   const float b = 2.0f * (d.x * o.x + d.y * o.y - k * d.z * (o.z - h));
   const float cc = o.x * o.x + o.y * o.y - k * (o.z - h) * (o.z - h);
@@ -439,11 +436,10 @@ D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   return t;
 }
 D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
-  const V3 pp = P3(p, 0), p1 = P3(p, 3), p2 = P3(p, 6);
+  const V3 pp = P3(p, 0);
   const float ah = p.a[9], ch = p.a[10];
-  {  // testBoundboxForHyperboloid :13-24
-    const float r1 = sqrtf_(p1.x * p1.x + p1.y * p1.y), r2 = sqrtf_(p2.x * p2.x + p2.y * p2.y);
-    const float rMax = fmax_(r1, r2), zMin = fmin_(p1.z, p2.z), zMax = fmax_(p1.z, p2.z);
+  {  // testBoundboxForHyperboloid :13-24 (rMax, zMin, zMax per scene)
+    const float rMax = p.a[11], zMin = p.a[12], zMax = p.a[13];
     if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
   }
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
@@ -453,7 +449,7 @@ D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
-  const float zMin = fmin_(p1.z, p2.z), zMax = fmax_(p1.z, p2.z);
+  const float zMin = p.a[12], zMax = p.a[13];
   if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
   if (hitOut) *hitOut = hit;
   return t;
@@ -464,7 +460,7 @@ D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const float zMin = fmin_(z0, z1), zMax = fmax_(z0, z1);
   if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
-  const float k = zMax / (rad * rad);
+  const float k = p.a[6];  // zMax / (rad * rad), per scene
   const float a = k * (d.x * d.x + d.y * d.y);
   const float b = 2.0f * k * (d.x * o.x + d.y * o.y) - d.z;
   const float cc = k * (o.x * o.x + o.y * o.y) - o.z;
@@ -498,16 +494,14 @@ D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dp
   h.dpdu = L2W(dpdu);
   h.dpdv = L2W(dpdv);
 }
-D void coneHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hit; coneT(p, r, &hit);
+D void coneHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
   const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
   const float vv = hit.z / hh;
   const V3 dpdv = v3(-hit.x / (1.0f - vv), -hit.y / (1.0f - vv), hh);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
-D void cylinderHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hit; cylinderT(p, r, &hit);
+D void cylinderHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
   const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
   finishLocal(c, p, hit, uv, dpduRot(hit), v3(0.0f, 0.0f, hh), h);
@@ -517,8 +511,7 @@ D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperbo
   dpdu = dpduRot(hit);
   dpdv = v3((p2.x - p1.x) * cosPhi - (p2.y - p1.y) * sinPhi, (p2.x - p1.x) * sinPhi + (p2.y - p1.y) * cosPhi, p2.z - p1.z);
 }
-D void hypHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hit; hypT(p, r, &hit);
+D void hypHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const V3 p1 = P3(p, 3), p2 = P3(p, 6);
   const float v = (hit.z - p1.z) / (p2.z - p1.z);
   const V3 pr = (1.0f - v) * p1 + v * p2;
@@ -532,16 +525,14 @@ D void paraDpD(V3 hit, float zMax, float zMin, V3& dpdu, V3& dpdv) {  // parabol
   dpdu = dpduRot(hit);
   dpdv = (zMax - zMin) * v3(hit.x / (2.0f * hit.z), hit.y / (2.0f * hit.z), 1.0f);
 }
-D void paraHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hit; paraT(p, r, &hit);
+D void paraHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
   const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), (hit.z - zMin) / (zMax - zMin)) : v2(0.0f, 0.0f);
   V3 dpdu, dpdv;
   paraDpD(hit, zMax, zMin, dpdu, dpdv);
   finishLocal(c, p, hit, uv, dpdu, dpdv, h);
 }
-D void diskHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
-  V3 hit; diskT(p, r, &hit);
+D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float rad = p.a[3], ri = p.a[4];
   const float dist2 = hit.x * hit.x + hit.y * hit.y;
   V2 uv = v2(0.0f, 0.0f);
@@ -554,16 +545,17 @@ D void diskHit(const Ctx& c, const SailPrim& p, const Ray& r, Hit& h) {
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
 
-D float primT(const SailPrim& p, const Ray& r) {
+// hl (may be null): the local-space hit point of the shapes whose hit record starts from it
+D float primT(const SailPrim& p, const Ray& r, V3* hl) {
   switch (p.type) {
     case SAIL_CUBE: return cubeT(p, r);
-    case SAIL_SPHERE: return sphereT(p, r, nullptr);
-    case SAIL_RECTANGLE: return rectT(p, r, nullptr);
-    case SAIL_CONE: return coneT(p, r, nullptr);
-    case SAIL_CYLINDER: return cylinderT(p, r, nullptr);
-    case SAIL_DISK: return diskT(p, r, nullptr);
-    case SAIL_HYPERBOLOID: return hypT(p, r, nullptr);
-    case SAIL_PARABOLOID: return paraT(p, r, nullptr);
+    case SAIL_SPHERE: return sphereT(p, r, hl);
+    case SAIL_RECTANGLE: return rectT(p, r, hl);
+    case SAIL_CONE: return coneT(p, r, hl);
+    case SAIL_CYLINDER: return cylinderT(p, r, hl);
+    case SAIL_DISK: return diskT(p, r, hl);
+    case SAIL_HYPERBOLOID: return hypT(p, r, hl);
+    case SAIL_PARABOLOID: return paraT(p, r, hl);
     case SAIL_CORNELLBOX: return cornellT(p, r);
     default: return kMaxDistance;
   }
@@ -573,7 +565,7 @@ D float primT(const SailPrim& p, const Ray& r) {
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   for (int i = 0; i < c.n; i++) {
-    const float t = primT(c.prims[i], r);
+    const float t = primT(c.prims[i], r, nullptr);
     if (t < best) {
       best = t;
       if (c.shadowAnyHit && best > kEps && best < kOneMinusEps) break;  // exact: no prim returns t <= EPSILON
@@ -582,14 +574,25 @@ D float closestT(const Ctx& c, const Ray& r) {
   return best;
 }
 
-// generated intersectObjects (shader.shape.js:28-51): t-only sweep, then one full record for the winner
+// generated intersectObjects (shader.shape.js:28-51): one sweep keeps the winner's distance and local hit
+// point, then one full record is built for the winner alone
 D Hit intersectObjects(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   int bi = -1;
+  V3 bhl = v3s(0.0f);
+#if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
-    const float t = primT(c.prims[i], r);
+    V3 hl = v3s(0.0f);
+    const float t = primT(c.prims[i], r, &hl);
+    if (t < best) { best = t; bi = i; bhl = hl; }
+  }
+#else
+  for (int i = 0; i < c.n; i++) {
+    const float t = primT(c.prims[i], r, nullptr);
     if (t < best) { best = t; bi = i; }
   }
+  if (bi >= 0) primT(c.prims[bi], r, &bhl);  // the same arithmetic again, for the winner only
+#endif
   Hit h;
   h.d = best;
   h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
@@ -598,13 +601,13 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   const SailPrim& p = c.prims[bi];
   switch (p.type) {
     case SAIL_CUBE: cubeHit(c, p, r, best, h); break;
-    case SAIL_SPHERE: sphereHit(c, p, r, h); break;
-    case SAIL_RECTANGLE: rectHit(c, p, r, h); break;
-    case SAIL_CONE: coneHit(c, p, r, h); break;
-    case SAIL_CYLINDER: cylinderHit(c, p, r, h); break;
-    case SAIL_DISK: diskHit(c, p, r, h); break;
-    case SAIL_HYPERBOLOID: hypHit(c, p, r, h); break;
-    case SAIL_PARABOLOID: paraHit(c, p, r, h); break;
+    case SAIL_SPHERE: sphereHit(c, p, bhl, h); break;
+    case SAIL_RECTANGLE: rectHit(c, p, bhl, h); break;
+    case SAIL_CONE: coneHit(c, p, bhl, h); break;
+    case SAIL_CYLINDER: cylinderHit(c, p, bhl, h); break;
+    case SAIL_DISK: diskHit(c, p, bhl, h); break;
+    case SAIL_HYPERBOLOID: hypHit(c, p, bhl, h); break;
+    case SAIL_PARABOLOID: paraHit(c, p, bhl, h); break;
     case SAIL_CORNELLBOX: cornellHit(p, r, best, h); break;
     default: break;
   }
@@ -636,9 +639,9 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
     case SAIL_RECTANGLE: {
       const V3 mn = P3(p, 0), mx = P3(p, 3);
       const V3 x = v3(mx.x - mn.x, 0.0f, 0.0f), y = v3(0.0f, mx.y - mn.y, mx.z - mn.z);
-      pdf = 1.0f / (length(x) * length(y));
+      pdf = p.a[17];                                   // 1 / (length(x) * length(y)), per scene
       const V3 res = mn + x * u.x + y * u.y;
-      normal = s * normalize(cross(x, y));
+      normal = s * P3(p, 6);                           // normalize(cross(x, y)) == the frame normal
       return res;
     }
     case SAIL_DISK: {
@@ -952,7 +955,13 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigne
     if (ins.d >= kMaxDistance) break;
     if (depth == 1) { n = ins.normal; p = ins.hit; }
     // shade()
+    // box faces have axis-aligned unit dpdu: dot == 1 exactly, sqrt(1) == 1 and v / 1 == v bit for bit
+#if SAIL_SS_UNIT
+    const float dd = dot(ins.dpdu, ins.dpdu);
+    const V3 ss = (dd == 1.0f) ? ins.dpdu : ins.dpdu / sqrtf_(dd), ts = cross(ins.normal, ss);
+#else
     const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
+#endif
     const V3 wo = worldToLocal(-ray.d, ins.normal, ss, ts);
     // the hash is evaluated only for materials that consume it (matte/metal/glass; mirror is deterministic)
     const V2 u2 = (ins.matCategory != SAIL_MIRROR) ? random2(c, seed) : v2(0.0f, 0.0f);

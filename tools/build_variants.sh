@@ -1,6 +1,7 @@
 #!/bin/sh
 # Builds experimental variants of libsail_hip.so (same sources, different -D flags) into sail_amd/lib/variants/.
 # Usage: tools/build_variants.sh name1 "-DFLAG=1" name2 "-DFLAG=2" ...
+# A flags string may start with "src=<file under csrc/>" to build that source instead of sail_trace.hip.
 set -e
 cd "$(dirname "$0")/../sail_amd"
 mkdir -p lib/variants build/variants
@@ -10,7 +11,9 @@ $HIPCC $COMMON -c csrc/sail_capi.cpp -o build/variants/sail_capi.o
 $HIPCC $COMMON -c csrc/sail_hostmath.cpp -o build/variants/sail_hostmath.o
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  $HIPCC $COMMON $flags -c csrc/sail_trace.hip -o build/variants/trace_$name.o
+  src=sail_trace.hip
+  case "$flags" in src=*) src=${flags%% *}; src=${src#src=}; flags=${flags#src=$src}; esac
+  $HIPCC $COMMON $flags -Icsrc -c csrc/$src -o build/variants/trace_$name.o
   $HIPCC -shared -fPIC --offload-arch=gfx950 build/variants/trace_$name.o build/variants/sail_capi.o \
     build/variants/sail_hostmath.o -o lib/variants/libsail_hip_$name.so -ldl
   echo "built $name ($flags)"
