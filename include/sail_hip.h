@@ -45,7 +45,12 @@ enum sail_accum_mode {
 /* multi-GPU partition of one frame (sail_set_partition) */
 enum sail_partition { SAIL_PART_TILES = 0, SAIL_PART_SAMPLES = 1 };
 /* display filters (Scene.filter, src/shader/filter/shader.filter.js:18-30) */
-enum sail_filter_kind { SAIL_FILTER_COLOR = 0, SAIL_FILTER_GAMMA = 1, SAIL_FILTER_TONEMAPPING = 2, SAIL_FILTER_WINDOW = 3 };
+enum sail_filter_kind {
+  SAIL_FILTER_COLOR = 0, SAIL_FILTER_GAMMA = 1, SAIL_FILTER_TONEMAPPING = 2, SAIL_FILTER_WINDOW = 3,
+  SAIL_FILTER_WAVELET = 4,  /* wavelet.glsl: a-trous over colour + position AOV (needs SAIL_FLAG_AOV) */
+  SAIL_FILTER_NORMAL = 5,   /* normal.glsl: the normal AOV (needs SAIL_FLAG_AOV) */
+  SAIL_FILTER_POSITION = 6  /* position.glsl: the position AOV (needs SAIL_FLAG_AOV) */
+};
 
 /* compiled plugin set (Scene.tracerConfig(), src/scene/scene.js:70-112), as bit masks over category ids:
  * shape bit = shape id (define.glsl:18-26), material bit = material id (:32-35), texture bit = texture id

@@ -1383,6 +1383,65 @@ int oracle_filter(const float* mean, int W, int H, int kind, const float* weight
   return 0;
 }
 
+// ---- AOV filters: wavelet.glsl:5-54 (a-trous), normal.glsl, position.glsl -------------------------------------------
+// mean, nrm, pos: W*H*4 maps (alpha ignored: RGB textures read alpha 1). kind 4 wavelet (FILTER_WAVELET_R = (rx, ry);
+// the 512 / 1280 texture-space constants generalise to W / 2.5 W), 5 normal, 6 position.
+int oracle_filter_aov(const float* mean, const float* nrm, const float* pos, int W, int H, int kind, float rx,
+                      float ry, float* out) {
+  if (!mean || !nrm || !pos || !out || W <= 0 || H <= 0 || kind < 4 || kind > 6) return -1;
+  const float hk[5] = {0.375f, 0.25f, 0.0625f, 0.0625f, 0.25f};          // wavelet.glsl:29
+  const float dW = (float)W, dH = (float)H, dW2 = dW * 2.5f, dH2 = dH * 2.5f;
+  for (int y = 0; y < H; y++) {
+    for (int x = 0; x < W; x++) {
+      const float tcx = ((float)x + 0.5f) / (float)W, tcy = ((float)y + 0.5f) / (float)H;
+      float* o = out + 4 * ((size_t)y * W + x);
+      if (kind == 5 || kind == 6) {
+        float m[3];
+        bilinear(kind == 5 ? nrm : pos, W, H, tcx, tcy, m);
+        o[0] = m[0]; o[1] = m[1]; o[2] = m[2]; o[3] = 1.0f;
+        continue;
+      }
+      float cval[4], pval[4];
+      bilinear(mean, W, H, tcx, tcy, cval); cval[3] = 1.0f;               // texture(colorMap, texCoord)
+      bilinear(pos, W, H, tcx, tcy, pval); pval[3] = 1.0f;
+      float color[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      float weightSum = 0.0f;
+      for (int n = 0; n < 3; n++) {
+        const float stepwidth = refm::pow_s(2.0f, (float)n) - 1.0f;
+        int count = 0;
+        for (int i = 0; i < 5; i++) {
+          for (int j = 0; j < 5; j++, count++) {
+            const int delt = abs(count - 12);
+            float h = 0.0f;
+            if (delt % (refm::to_int(stepwidth) + 1) == 0) h = hk[(delt / (refm::to_int(stepwidth) + 1)) % 5];
+            if (h == 0.0f) continue;
+            const float u = (tcx - rx / dW) + ((float)j + 0.5f) * rx / dW2;
+            const float v = (tcy - ry / dH) + ((float)i + 0.5f) * ry / dH2;
+            // W() :5-22
+            float ctmp[4], ptmp[4], t[4];
+            bilinear(mean, W, H, u, v, ctmp); ctmp[3] = 1.0f;
+            for (int k = 0; k < 4; k++) t[k] = cval[k] - ctmp[k];
+            float dist2 = t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+            const float c_w = refm::fmin_s(refm::exp_s(-(dist2) / 4.0f), 1.0f);
+            dist2 = refm::fmax_s((t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3]) / (stepwidth * stepwidth), 0.0f);
+            const float n_w = refm::fmin_s(refm::exp_s(-(dist2) / 128.0f), 1.0f);
+            bilinear(pos, W, H, u, v, ptmp); ptmp[3] = 1.0f;
+            for (int k = 0; k < 4; k++) t[k] = pval[k] - ptmp[k];
+            dist2 = t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
+            const float p_w = refm::fmin_s(refm::exp_s(-(dist2) / 1.0f), 1.0f);
+            const float weight = c_w * n_w * p_w * h;
+            for (int k = 0; k < 4; k++) ctmp[k] *= weight;
+            weightSum += weight;
+            for (int k = 0; k < 4; k++) color[k] += ctmp[k];
+          }
+        }
+      }
+      for (int k = 0; k < 4; k++) o[k] = color[k] / weightSum;
+    }
+  }
+  return 0;
+}
+
 // ---- exported spec math for the GPU bit-parity test ----------------------------------------------------------
 void oracle_math(int fn, const float* x, const float* y, float* out, int count) {
   for (int i = 0; i < count; i++) {

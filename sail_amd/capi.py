@@ -21,6 +21,7 @@ FLAG_SEGMENT_COUNT = 2
 ACCUM_SUM, ACCUM_MIX, ACCUM_COMPAT8 = 0, 1, 2
 PART_TILES, PART_SAMPLES = 0, 1
 FILTER_COLOR, FILTER_GAMMA, FILTER_TONEMAPPING, FILTER_WINDOW = 0, 1, 2, 3
+FILTER_WAVELET, FILTER_NORMAL, FILTER_POSITION = 4, 5, 6  # need FLAG_AOV
 
 # exported symbols (kept in sync with include/sail_hip.h; tests/test_capi_symbols.py checks both ways)
 EXPORTS = (

@@ -88,6 +88,8 @@ struct sail_ctx {
   float4* accum = nullptr;
   float4* aovN = nullptr;
   float4* aovP = nullptr;
+  float4* filterOut = nullptr;    // display-filter outputs, allocated on first use
+  uint8_t* filterOut8 = nullptr;
   unsigned long long* segCounter = nullptr;
   SailPrim* prims = nullptr;
   float* tp = nullptr;
@@ -409,7 +411,7 @@ void sail_destroy(sail_ctx* c) {
   if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
   for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->evPool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->accum, c->aovN, c->aovP, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
+  void* bufs[] = {c->accum, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -573,19 +575,27 @@ int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
 
 int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float ry, float gammaC, float* out, uint8_t* out8) {
   if (!c) return SAIL_E_INVALID;
-  if (kind < SAIL_FILTER_COLOR || kind > SAIL_FILTER_WINDOW || (kind == SAIL_FILTER_WINDOW && !weights16))
+  if (kind < SAIL_FILTER_COLOR || kind > SAIL_FILTER_POSITION || (kind == SAIL_FILTER_WINDOW && !weights16))
     return fail(c, SAIL_E_INVALID, "sail_filter: kind %d", kind);
+  if (kind >= SAIL_FILTER_WAVELET && !c->aovN)
+    return fail(c, SAIL_E_STATE, "sail_filter: kind %d reads the AOVs (create with SAIL_FLAG_AOV)", kind);
   HIPCHK(c, hipSetDevice(c->device));
   int rc = sail_sync(c);
   if (rc) return rc;
   const size_t np = (size_t)c->W * c->H;
-  float4* dOut = nullptr;
-  uint8_t* dOut8 = nullptr;
-  if (out && hipMalloc(&dOut, np * sizeof(float4)) != hipSuccess) return fail(c, SAIL_E_OOM, "filter output");
-  if (out8 && hipMalloc(&dOut8, np * 4) != hipSuccess) { if (dOut) (void)hipFree(dOut); return fail(c, SAIL_E_OOM, "filter output"); }
+  if (out && !c->filterOut && hipMalloc(&c->filterOut, np * sizeof(float4)) != hipSuccess) {
+    c->filterOut = nullptr;
+    return fail(c, SAIL_E_OOM, "filter output");
+  }
+  if (out8 && !c->filterOut8 && hipMalloc(&c->filterOut8, np * 4) != hipSuccess) {
+    c->filterOut8 = nullptr;
+    return fail(c, SAIL_E_OOM, "filter output");
+  }
+  float4* dOut = out ? c->filterOut : nullptr;
+  uint8_t* dOut8 = out8 ? c->filterOut8 : nullptr;
   SailFilterArgs A;
   memset(&A, 0, sizeof A);
-  A.accum = c->accum; A.out = dOut; A.out8 = dOut8; A.W = c->W; A.H = c->H; A.kind = kind; A.accumMode = c->accumMode;
+  A.accum = c->accum; A.aovN = c->aovN; A.aovP = c->aovP; A.out = dOut; A.out8 = dOut8; A.W = c->W; A.H = c->H; A.kind = kind; A.accumMode = c->accumMode;
   // a SUM accumulator holds the same count in every pixel of a frame (all pixels get every sample)
   float cnt = 1.0f;
   if (c->accumMode == SAIL_ACCUM_SUM) {
@@ -600,8 +610,6 @@ int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float r
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess && out) e = hipMemcpy(out, dOut, np * sizeof(float4), hipMemcpyDeviceToHost);
   if (e == hipSuccess && out8) e = hipMemcpy(out8, dOut8, np * 4, hipMemcpyDeviceToHost);
-  if (dOut) (void)hipFree(dOut);
-  if (dOut8) (void)hipFree(dOut8);
   if (e != hipSuccess) return fail(c, SAIL_E_HIP, "sail_filter: %s", hipGetErrorString(e));
   return SAIL_OK;
 }

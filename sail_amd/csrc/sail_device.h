@@ -63,10 +63,12 @@ struct SailTraceArgs {
 
 struct SailFilterArgs {
   const float4* accum;
+  const float4* aovN;       // normalMap (kinds 4-5)
+  const float4* aovP;       // positionMap (kinds 4, 6)
   float4* out;
   uint8_t* out8;
   int W, H;
-  int kind;                 // 0 color, 1 gamma, 2 tonemapping, 3 window
+  int kind;                 // 0 color, 1 gamma, 2 tonemapping, 3 window, 4 wavelet, 5 normal, 6 position
   int accumMode;
   float invCount;           // unused for mix modes
   float count;

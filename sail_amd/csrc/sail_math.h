@@ -153,6 +153,7 @@ SM_D float powf_(float x, float y) {
   if (x == 0.0f) return (y > 0.0f) ? 0.0f : __builtin_inff();
   return (float)exp_d((double)y * log_d((double)x));
 }
+SM_D float expf_(float x) { return (float)exp_d((double)x); }  // wavelet weights only
 // GLSL min/max/clamp: the hardware v_min_f32/v_max_f32 (a NaN operand yields the other; -0 < +0)
 SM_D float fmin_(float a, float b) { return __builtin_fminf(a, b); }
 SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }

@@ -1065,36 +1065,45 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_tra
 }
 
 // ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
+// Every map is sampled as the reference's frame textures are: LINEAR, default REPEAT wrap (webgl.js:153-156),
+// RGB (texture() returns alpha 1). The colour map is the mean image (SUM accumulators divided per texel).
 namespace {
 D int wrapi(int i, int size) { int m = i % size; return m < 0 ? m + size : m; }
-D float meanC(const SailFilterArgs& A, int xi, int yi, int ch) {
-  const float4 v = A.accum[(size_t)yi * A.W + xi];
-  const float comp = ch == 0 ? v.x : (ch == 1 ? v.y : v.z);
-  return A.accumMode == 0 ? comp / A.count : comp;
-}
-D void bilinear(const SailFilterArgs& A, float u, float v, float out[3]) {
-  const float fx = u * (float)A.W - 0.5f, fy = v * (float)A.H - 0.5f;
+struct Tap { int xa, xb, ya, yb; float a, b; };
+D Tap tapAt(int W, int H, float u, float v) {
+  const float fx = u * (float)W - 0.5f, fy = v * (float)H - 0.5f;
   const float x0f = floorf(fx), y0f = floorf(fy);
-  const float a = fx - x0f, b = fy - y0f;
+  Tap t;
+  t.a = fx - x0f; t.b = fy - y0f;
   const int xi = (int)x0f, yi = (int)y0f;
-  const int xa = wrapi(xi, A.W), xb = wrapi(xi + 1, A.W), ya = wrapi(yi, A.H), yb = wrapi(yi + 1, A.H);
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    const float t00 = meanC(A, xa, ya, c), t10 = meanC(A, xb, ya, c), t01 = meanC(A, xa, yb, c), t11 = meanC(A, xb, yb, c);
-    const float c0 = t00 * (1.0f - a) + t10 * a, c1 = t01 * (1.0f - a) + t11 * a;
-    out[c] = c0 * (1.0f - b) + c1 * b;
-  }
+  t.xa = wrapi(xi, W); t.xb = wrapi(xi + 1, W); t.ya = wrapi(yi, H); t.yb = wrapi(yi + 1, H);
+  return t;
 }
+D V3 texel(const SailFilterArgs& A, const float4* img, bool mean, int x, int y) {
+  const float4 v = img[(size_t)y * A.W + x];
+  if (mean && A.accumMode == 0) return v3(v.x / A.count, v.y / A.count, v.z / A.count);
+  return v3(v.x, v.y, v.z);
+}
+D V3 bilerp(V3 t00, V3 t10, V3 t01, V3 t11, float a, float b) {
+  const V3 c0 = t00 * (1.0f - a) + t10 * a, c1 = t01 * (1.0f - a) + t11 * a;
+  return c0 * (1.0f - b) + c1 * b;
+}
+D V3 sample(const SailFilterArgs& A, const float4* img, bool mean, float u, float v) {
+  const Tap t = tapAt(A.W, A.H, u, v);
+  return bilerp(texel(A, img, mean, t.xa, t.ya), texel(A, img, mean, t.xb, t.ya), texel(A, img, mean, t.xa, t.yb),
+                texel(A, img, mean, t.xb, t.yb), t.a, t.b);
+}
+D float dot4(V3 t, float w) { return t.x * t.x + t.y * t.y + t.z * t.z + w * w; }
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterArgs A) {
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
   if (x >= A.W || y >= A.H) return;
   const float tcx = ((float)x + 0.5f) / (float)A.W, tcy = ((float)y + 0.5f) / (float)A.H;
-  float o[3];
-  if (A.kind == 0 || A.kind == 1 || A.kind == 2) {
-    float col[3];
-    bilinear(A, tcx, tcy, col);
+  float o[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  if (A.kind <= 2) {  // color.glsl / gamma.glsl / tonemapping.glsl
+    const V3 cv = sample(A, A.accum, true, tcx, tcy);
+    const float col[3] = {cv.x, cv.y, cv.z};
     for (int c = 0; c < 3; c++) {
       if (A.kind == 0) o[c] = col[c];
       else if (A.kind == 1) o[c] = powf_(col[c], 1.0f / A.gammaC);
@@ -1103,33 +1112,70 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
         o[c] = (xx * (6.2f * xx + 0.5f)) / (xx * (6.2f * xx + 1.7f) + 0.06f);
       }
     }
-  } else {
-    float acc[3] = {0.0f, 0.0f, 0.0f};
+  } else if (A.kind == 3) {  // window.glsl:1-44, FILTER_WINDOW_WIDTH 4
+    V3 acc = v3s(0.0f);
     float weightSum = 0.0f;
     for (int i = 0; i < 4; i++) {
       for (int j = 0; j < 4; j++) {
         const float wi = ((float)j + 0.5f) * A.rx / 4.0f, wj = ((float)i + 0.5f) * A.ry / 4.0f;
         const float ox = wi / (float)A.W, oy = wj / (float)A.H;
-        float tmp[3] = {0.0f, 0.0f, 0.0f};
+        V3 tmp = v3s(0.0f);
         int count = 0;
         for (int q = 0; q < 4; q++) {
           const float u = (q < 2) ? tcx + ox : tcx - ox;
           const float v = (q & 1) ? tcy - oy : tcy + oy;
           if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) continue;
           count++;
-          float s3[3];
-          bilinear(A, u, v, s3);
-          tmp[0] += s3[0]; tmp[1] += s3[1]; tmp[2] += s3[2];
+          tmp = tmp + sample(A, A.accum, true, u, v);
         }
         const float weight = A.weights[i * j + j];
         weightSum += weight * (float)count;
-        acc[0] += tmp[0] * weight; acc[1] += tmp[1] * weight; acc[2] += tmp[2] * weight;
+        acc = acc + tmp * weight;
       }
     }
-    o[0] = acc[0] / weightSum; o[1] = acc[1] / weightSum; o[2] = acc[2] / weightSum;
+    o[0] = acc.x / weightSum; o[1] = acc.y / weightSum; o[2] = acc.z / weightSum;
+  } else if (A.kind == 4) {  // wavelet.glsl:5-54 (edge-avoiding a-trous over the colour and position maps)
+    const V3 cval = sample(A, A.accum, true, tcx, tcy);
+    const V3 pval = sample(A, A.aovP, false, tcx, tcy);
+    // the reference reads normalMap (nval, ntmp) but never uses it: its "normal" weight reuses the colour
+    // difference (wavelet.glsl:11-12)
+    const float hk[5] = {0.375f, 0.25f, 0.0625f, 0.0625f, 0.25f};
+    const float dW = (float)A.W, dH = (float)A.H, dW2 = dW * 2.5f, dH2 = dH * 2.5f;  // 512, 1280 at 512^2
+    float col[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float weightSum = 0.0f;
+    for (int n = 0; n < 3; n++) {
+      const float stepwidth = powf_(2.0f, (float)n) - 1.0f;
+      const int div = to_int(stepwidth) + 1;
+      int count = 0;
+      for (int i = 0; i < 5; i++) {
+        for (int j = 0; j < 5; j++, count++) {
+          const int delt = abs(count - 12);
+          float h = 0.0f;
+          if (delt % div == 0) h = hk[(delt / div) % 5];
+          if (h == 0.0f) continue;
+          const float u = (tcx - A.rx / dW) + ((float)j + 0.5f) * A.rx / dW2;
+          const float v = (tcy - A.ry / dH) + ((float)i + 0.5f) * A.ry / dH2;
+          const V3 ctmp = sample(A, A.accum, true, u, v);
+          const V3 t = cval - ctmp;
+          const float tw = 1.0f - 1.0f;
+          const float c_w = fmin_(expf_(-(dot4(t, tw)) / 4.0f), 1.0f);
+          const float d2 = fmax_(dot4(t, tw) / (stepwidth * stepwidth), 0.0f);
+          const float n_w = fmin_(expf_(-(d2) / 128.0f), 1.0f);
+          const V3 tp = pval - sample(A, A.aovP, false, u, v);
+          const float p_w = fmin_(expf_(-(dot4(tp, tw)) / 1.0f), 1.0f);
+          const float weight = c_w * n_w * p_w * h;
+          weightSum += weight;
+          col[0] += ctmp.x * weight; col[1] += ctmp.y * weight; col[2] += ctmp.z * weight; col[3] += 1.0f * weight;
+        }
+      }
+    }
+    for (int c = 0; c < 4; c++) o[c] = col[c] / weightSum;
+  } else {  // normal.glsl / position.glsl: the AOV map at the texel
+    const V3 m = sample(A, A.kind == 5 ? A.aovN : A.aovP, false, tcx, tcy);
+    o[0] = m.x; o[1] = m.y; o[2] = m.z;
   }
   const size_t pix = (size_t)y * A.W + x;
-  if (A.out) A.out[pix] = make_float4(o[0], o[1], o[2], 1.0f);
+  if (A.out) A.out[pix] = make_float4(o[0], o[1], o[2], o[3]);
   if (A.out8) {
     for (int c = 0; c < 3; c++) A.out8[4 * pix + c] = (uint8_t)(int)(fmin_(fmax_(o[c], 0.0f), 1.0f) * 255.0f + 0.5f);
     A.out8[4 * pix + 3] = 255;

@@ -5,7 +5,7 @@
 // sampled at ((j+.5) r_x/4, (i+.5) r_y/4) from the one-decimal getParam() values, while the window radius
 // itself is the raw FILTER_WINDOW_RADIUS text (e.g. "vec2(2.0,2.0)") evaluated as GLSL would.
 
-const KIND = { color: 0, gamma: 1, tonemapping: 2, window: 3 };
+const KIND = { color: 0, gamma: 1, tonemapping: 2, window: 3, wavelet: 4, normal: 5, position: 6 };
 const WINDOW = 4;
 
 function gaussianW(d, expv, alpha) { return Math.max(0.0, Math.exp(-alpha * d * d) - expv); }
@@ -67,8 +67,14 @@ function filterConfig(pp) {
       const w64 = windowWeights(pp);
       return { kind: KIND.window, weights: Float32Array.from(w64), weights64: w64, rx, ry, gamma: 1 };
     }
-    case 'normal': case 'position': return { kind: KIND.color, aov: pp.name, weights: null, rx: 0, ry: 0, gamma: 1 };
-    default: throw new Error(`filter "${pp.name}" is not supported by this build (wavelet: SURVEY §8(f) next)`);
+    // the AOV filters (normal.glsl, position.glsl, wavelet.glsl) need a Renderer created with aov: true
+    case 'normal': case 'position': return { kind: KIND[pp.name], aov: true, weights: null, rx: 0, ry: 0, gamma: 1 };
+    case 'wavelet': {
+      if (pp.params.r === undefined) throw new Error("wavelet filter needs scene.filter.addParam('r', 'vec2(x,y)')");
+      const [rx, ry] = glslVec2(pp.params.r);  // FILTER_WAVELET_R (wavelet.glsl:42-44)
+      return { kind: KIND.wavelet, aov: true, weights: null, rx, ry, gamma: 1 };
+    }
+    default: throw new Error(`filter "${pp.name}" is not a Sail display filter`);
   }
 }
 

@@ -98,13 +98,7 @@ class Renderer {
   // the display pass: pixelFilter over the accumulated frame -> RGBA8 (row 0 = bottom, GL order)
   image() {
     const f = this.filter;
-    if (f.aov) {
-      const rb = this.lib.readback(this.ctx, true);
-      const src = f.aov === 'normal' ? rb.normal : rb.position;
-      const out = new Uint8Array(src.length);
-      for (let i = 0; i < src.length; i++) out[i] = Math.floor(Math.min(Math.max(src[i], 0), 1) * 255 + 0.5);
-      return out;
-    }
+    if (f.aov && !this.aov) throw new Error('this display filter reads the AOVs: create the Renderer with aov: true');
     return this.lib.filter(this.ctx, f.kind, f.weights, f.rx, f.ry, f.gamma).rgba8;
   }
 

@@ -1,18 +1,28 @@
 'use strict';
 // Renders a frozen scene through Sail.Renderer -> N-API -> libsail_hip.so and writes the raw accumulator
 // (and the canvas pixels) for tests/test_js_host.py to compare with the CPU oracle. Needs an MI355X.
-// argv: scene W H spp bounces mode(sum|mix) api(samples|frames) out_prefix
+// argv: scene W H spp bounces mode(sum|mix) api(samples|frames) out_prefix [filter [filter-r]]
 const fs = require('fs');
 const Sail = require('../../sail_amd/js');
 const { SCENES } = require('../../sail_amd/js/scenes');
-const [name, W, H, spp, B, mode, api, out] = process.argv.slice(2);
+const [name, W, H, spp, B, mode, api, out, filter, filterR] = process.argv.slice(2);
 const scene = SCENES[name]();
+if (filter) {  // the reference's scene.filter = name; scene.filter.addParam('r', ...) flow
+  scene.filter = filter;
+  if (filterR) scene.filter.addParam('r', filterR);
+}
 const r = new Sail.Renderer({ width: +W, height: +H, deterministic: true, accumulation: mode, maxBounces: +B, display: false });
 r.update(scene);
 if (api === 'samples') r.renderSamples(scene, +spp);
 else for (let i = 0; i < +spp; i++) r.render(scene);
 fs.writeFileSync(out + '.accum.f32', Buffer.from(r.readAccum().buffer));
 fs.writeFileSync(out + '.rgba8', Buffer.from(r.image().buffer));
+if (filter) {
+  const rb = r.lib.readback(r.ctx, true);
+  fs.writeFileSync(out + '.mean.f32', Buffer.from(rb.rgba.buffer));
+  fs.writeFileSync(out + '.normal.f32', Buffer.from(rb.normal.buffer));
+  fs.writeFileSync(out + '.position.f32', Buffer.from(rb.position.buffer));
+}
 const st = r.stats();
 fs.writeFileSync(out + '.stats.json', JSON.stringify(st));
 r.destroy();

@@ -39,6 +39,8 @@ def lib(count: bool = False) -> ctypes.CDLL:
                                 f32p, f32p, f32p, ci, ci, ci, ci, f32p, f32p, f32p]
     L.oracle_filter.restype = ci
     L.oracle_filter.argtypes = [f32p, ci, ci, ci, f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p]
+    L.oracle_filter_aov.restype = ci
+    L.oracle_filter_aov.argtypes = [f32p, f32p, f32p, ci, ci, ci, ctypes.c_float, ctypes.c_float, f32p]
     L.oracle_math.restype = None
     L.oracle_math.argtypes = [ci, f32p, f32p, f32p, ci]
     L.oracle_intersect_t.restype = ctypes.c_float
@@ -89,6 +91,18 @@ def filter_image(mean: np.ndarray, kind: int, weights16=None, rx=0.0, ry=0.0, ga
     rc = L.oracle_filter(_p(m), W, H, kind, _p(w), rx, ry, gamma_c, _p(out))
     if rc:
         raise RuntimeError(f"oracle_filter: {rc}")
+    return out
+
+
+def filter_aov(mean: np.ndarray, normal: np.ndarray, position: np.ndarray, kind: int, rx=0.0, ry=0.0) -> np.ndarray:
+    """wavelet (4) / normal (5) / position (6) display filters over the mean image and the AOV maps"""
+    L = lib()
+    H, W = mean.shape[:2]
+    m, n, p = _f(mean), _f(normal), _f(position)
+    out = np.zeros((H, W, 4), dtype=np.float32)
+    rc = L.oracle_filter_aov(_p(m), _p(n), _p(p), W, H, kind, rx, ry, _p(out))
+    if rc:
+        raise RuntimeError(f"oracle_filter_aov: {rc}")
     return out
 
 

@@ -228,3 +228,32 @@ def test_update_objects_and_reset(gpu, fixtures):
     sc2 = dict(sc, objects=moved.reshape(-1).tolist())
     want = oracle.render(sc2, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], 4)
     assert bit_equal(got, want).all()
+
+
+# ---- AOV display filters: wavelet.glsl (a-trous), normal.glsl, position.glsl ------------------------------------
+@pytest.mark.parametrize("kind,r", [(capi.FILTER_WAVELET, (2.0, 2.0)), (capi.FILTER_WAVELET, (3.5, 1.25)),
+                                    (capi.FILTER_NORMAL, (0.0, 0.0)), (capi.FILTER_POSITION, (0.0, 0.0))])
+def test_aov_filters_bit_exact(gpu, fixtures, kind, r):
+    sc = fixtures["scenes"]["C3"]
+    W, H, spp, B = 41, 35, 3, 5
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    ctx = capi.Context(W, H, flags=capi.FLAG_AOV)
+    ctx.set_scene_dict(sc)
+    ctx.render_schedule(inv, seeds, sc["eye"], B)
+    got, got8 = ctx.filter(kind, None, r[0], r[1], 2.2, want_u8=True)
+    mean, nrm, pos = ctx.readback(aov=True)
+    ctx.close()
+    want = oracle.filter_aov(mean, nrm, pos, kind, r[0], r[1])
+    assert bit_equal(got, want).all()
+    want8 = np.floor(np.clip(want[..., :3], 0, 1) * 255.0 + 0.5).astype(np.uint8)
+    assert (got8[..., :3] == want8).all()
+    if kind == capi.FILTER_WAVELET:
+        assert np.isfinite(got).all()
+
+
+def test_aov_filter_needs_aov_flag(gpu, fixtures):
+    ctx = capi.Context(8, 8)
+    ctx.set_scene_dict(fixtures["scenes"]["C1"])
+    with pytest.raises(RuntimeError):
+        ctx.filter(capi.FILTER_WAVELET, None, 2.0, 2.0)
+    ctx.close()

@@ -96,3 +96,24 @@ def test_js_renderer_bit_exact_vs_oracle(tmp_path, fixtures, exported, name, W, 
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
     rgba8 = np.fromfile(prefix + ".rgba8", dtype=np.uint8).reshape(H, W, 4)
     assert rgba8[..., 3].min() == 255
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flt,r,kind", [("wavelet", "vec2(2.0,2.0)", capi.FILTER_WAVELET),
+                                        ("normal", None, capi.FILTER_NORMAL), ("position", None, capi.FILTER_POSITION)])
+def test_js_aov_display_filters(tmp_path, flt, r, kind):
+    """scene.filter = 'wavelet' / 'normal' / 'position' through Renderer.image() -> sail_filter on the GPU,
+    checked against the oracle's filter over the same mean image and AOV maps"""
+    if capi.device_count() < 1:
+        pytest.skip("no HIP device")
+    W, H = 36, 28
+    prefix = str(tmp_path / flt)
+    args = [NODE, os.path.join(ROOT, "tests", "js", "render_check.js"), "C3", str(W), str(H), "3", "5", "sum", "samples",
+            prefix, flt] + ([r] if r else [])
+    subprocess.run(args, cwd=ROOT, check=True, timeout=300)
+    rd = {k: np.fromfile(f"{prefix}.{k}.f32", dtype=np.float32).reshape(H, W, 4) for k in ("mean", "normal", "position")}
+    rgba8 = np.fromfile(prefix + ".rgba8", dtype=np.uint8).reshape(H, W, 4)
+    rx = ry = 2.0 if r else 0.0
+    want = oracle.filter_aov(rd["mean"], rd["normal"], rd["position"], kind, rx, ry)
+    want8 = np.floor(np.clip(want[..., :3], 0, 1) * 255.0 + 0.5).astype(np.uint8)
+    assert (rgba8[..., :3] == want8).all()
