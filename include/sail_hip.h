@@ -105,6 +105,11 @@ int sail_read_accum(sail_ctx* ctx, float* rgba);
 /* RenderShader.render (src/core/renderer.js:63) -> pixelFilter (src/shader/filter/<kind>.glsl):
  * out_rgba = W*H*4 f32 (may be NULL), out_rgba8 = W*H*4 UNORM8 canvas pixels (may be NULL).
  * weights16 = the 16-entry window table (window filters), radius (rx, ry) in pixels, gamma_c for GAMMA. */
+/* Pickup.pick (src/core/pickup.js:46-66) on the GPU: for each of `count` rays (origin xyz, direction xyz;
+ * f32, 6 per ray) the trace kernel's own primitive sweep returns the first object row with the smallest
+ * distance (-1 on a miss) and that distance (1e5 = MAX_DISTANCE on a miss). Replaces the reference's f64 CPU
+ * picker (geometry.js intersect(), whose Rectangle test has the wrong plane) with the shader's intersection. */
+int sail_pick(sail_ctx* ctx, const float* rays, int count, int32_t* index, float* t);
 int sail_filter(sail_ctx* ctx, int kind, const float* weights16, float rx, float ry, float gamma_c,
                 float* out_rgba, uint8_t* out_rgba8);
 int sail_get_stats(sail_ctx* ctx, sail_stats* out);

@@ -1474,6 +1474,21 @@ float oracle_intersect_t(const float* objects, int n, const float* texparams, in
   return raw(ins.d);
 }
 
+// picking with the shader's intersectObjects (shader.shape.js:28-51): first row with the smallest d, -1 on a miss
+int oracle_pick(const float* objects, int n, const float* texparams, int tn, unsigned shape_mask, const float* rays,
+                int count, int* index, float* t) {
+  C.objects.d = objects; C.objects.w = 18; C.objects.h = n;
+  C.texParams.d = texparams; C.texParams.w = 16; C.texParams.h = tn;
+  C.n = n; C.tn = tn; C.shapeMask = shape_mask; C.texMask = 0xffffffffu;
+  for (int i = 0; i < count; i++) {
+    const float* q = rays + 6 * i;
+    const Intersect ins = intersectObjects(ray_(v3(F(q[0]), F(q[1]), F(q[2])), v3(F(q[3]), F(q[4]), F(q[5]))));
+    t[i] = raw(ins.d);
+    index[i] = ins.d < F(kMaxDistance) ? ins.index : -1;
+  }
+  return 0;
+}
+
 }  // extern "C"
 
 // ---- unit probes of individual restated functions (known-answer tests) ----------------------------------------

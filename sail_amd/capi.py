@@ -30,7 +30,7 @@ EXPORTS = (
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
-    "sail_math_probe",
+    "sail_math_probe", "sail_pick",
     "sail_abi_version",
 )
 
@@ -112,6 +112,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
                                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
         "sail_math_probe": (ctypes.c_int, [ctypes.c_int, f32p, f32p, f32p, ctypes.c_int]),
         "sail_abi_version": (ctypes.c_int, []),
+        "sail_pick": (ctypes.c_int, [vp, f32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), f32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -287,6 +288,14 @@ class Context:
         self._check(self.lib.sail_filter(self.h, kind, _ptr(w), rx, ry, gamma_c, _ptr(out),
                                          _ptr(out8, ctypes.c_uint8)), "sail_filter")
         return (out, out8) if want_u8 else out
+
+    def pick(self, rays) -> tuple:
+        """rays: (count, 6) origin+direction -> (object row index or -1, distance) per ray"""
+        r = _f32(rays).reshape(-1, 6)
+        idx = np.zeros(len(r), dtype=np.int32)
+        t = np.zeros(len(r), dtype=np.float32)
+        self._check(self.lib.sail_pick(self.h, _ptr(r), len(r), _ptr(idx, ctypes.c_int32), _ptr(t)), "sail_pick")
+        return idx, t
 
     def stats(self) -> Stats:
         s = Stats()

@@ -16,6 +16,8 @@
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
+hipError_t sail_launch_pick(const SailPrim* prims, int n, const float* rays, int count, int32_t* index, float* t,
+                            hipStream_t s);
 
 namespace {
 
@@ -611,6 +613,30 @@ int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float r
   if (e == hipSuccess && out) e = hipMemcpy(out, dOut, np * sizeof(float4), hipMemcpyDeviceToHost);
   if (e == hipSuccess && out8) e = hipMemcpy(out8, dOut8, np * 4, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(c, SAIL_E_HIP, "sail_filter: %s", hipGetErrorString(e));
+  return SAIL_OK;
+}
+
+int sail_pick(sail_ctx* c, const float* rays, int count, int32_t* index, float* t) {
+  if (!c || count < 0 || (count > 0 && (!rays || !index || !t))) return SAIL_E_INVALID;
+  if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_pick: no scene (call sail_set_scene first)");
+  if (count == 0) return SAIL_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = sail_sync(c);
+  if (rc) return rc;
+  float* dRays = nullptr;
+  void* dOut = nullptr;
+  if (hipMalloc(&dRays, (size_t)count * 6 * sizeof(float)) != hipSuccess) return fail(c, SAIL_E_OOM, "pick rays");
+  if (hipMalloc(&dOut, (size_t)count * 8) != hipSuccess) { (void)hipFree(dRays); return fail(c, SAIL_E_OOM, "pick out"); }
+  int32_t* dIdx = (int32_t*)dOut;
+  float* dT = (float*)((char*)dOut + (size_t)count * 4);
+  hipError_t e = hipMemcpyAsync(dRays, rays, (size_t)count * 6 * sizeof(float), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = sail_launch_pick(c->prims, c->n, dRays, count, dIdx, dT, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(index, dIdx, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(t, dT, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(dRays);
+  (void)hipFree(dOut);
+  if (e != hipSuccess) return fail(c, SAIL_E_HIP, "sail_pick: %s", hipGetErrorString(e));
   return SAIL_OK;
 }
 

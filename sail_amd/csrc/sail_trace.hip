@@ -1182,6 +1182,24 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
   }
 }
 
+// ---- picking (replaces the CPU picker, src/core/pickup.js:46-66): the trace kernel's own primitive sweep
+// for caller-supplied rays; index = the first object row with the smallest distance, -1 on a miss ---------------
+extern "C" __global__ void __launch_bounds__(64) sail_pick_kernel(const SailPrim* prims, int n, const float* rays,
+                                                                   int count, int32_t* index, float* tOut) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const float* q = rays + 6 * (size_t)i;
+  const Ray r = mkRay(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]));
+  float best = kMaxDistance;
+  int bi = -1;
+  for (int k = 0; k < n; k++) {
+    const float t = primT(prims[k], r, nullptr);
+    if (t < best) { best = t; bi = k; }
+  }
+  index[i] = bi;
+  tOut[i] = best;
+}
+
 // ---- spec-math probe for the CPU/GPU bit-parity test ----------------------------------------------------------------
 extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float* y, float* out, int count) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1213,6 +1231,11 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
 }
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s) {
   hipLaunchKernelGGL(sail_filter_kernel, dim3((A.W + 15) / 16, (A.H + 15) / 16), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_pick(const SailPrim* prims, int n, const float* rays, int count, int32_t* index, float* t,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(sail_pick_kernel, dim3((count + 63) / 64), dim3(64), 0, s, prims, n, rays, count, index, t);
   return hipGetLastError();
 }
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count) {

@@ -5,13 +5,7 @@ const scene = require('./src/scene');
 const { Vector, Matrix } = require('./src/la');
 const { Renderer } = require('./src/renderer');
 
-// Sail.Control wires mouse orbit/pick handlers to a browser canvas (src/core/control.js); the picking UI
-// is out of scope for this build (SURVEY §2 row 15), so the class keeps the call surface as no-ops.
-class Control {
-  constructor() {}
-  static init() {}
-  static update() {}
-}
+const { Control } = require('./src/control');  // mouse orbit / zoom / GPU pick + drag (control.js, pickup.js)
 
 const Sail = {
   Renderer,

@@ -282,6 +282,25 @@ napi_value Filter(napi_env env, napi_callback_info info) {  // (ctx, kind, weigh
   NAPI_OK(napi_set_named_property(env, out, "rgba8", u8));
   return out;
 }
+napi_value Pick(napi_env env, napi_callback_info info) {  // (ctx, Float32Array rays[6*count]) -> {index, t}
+  napi_value a[2];
+  if (!args(env, info, 2, a)) return nullptr;
+  Handle* h;
+  float* rays;
+  size_t nr;
+  if (!getHandle(env, a[0], &h) || !getArray(env, a[1], napi_float32_array, &rays, &nr)) return nullptr;
+  if (nr % 6) { napi_throw_range_error(env, nullptr, "rays need 6 floats each"); return nullptr; }
+  const size_t count = nr / 6;
+  void *pi = nullptr, *pt = nullptr;
+  napi_value idx = makeTyped(env, napi_int32_array, count, 4, &pi), t = makeTyped(env, napi_float32_array, count, 4, &pt);
+  const int rc = sail_pick(h->ctx, rays, (int)count, (int32_t*)pi, (float*)pt);
+  if (rc) return throwSail(env, "sail_pick", rc, h->ctx);
+  napi_value out;
+  NAPI_OK(napi_create_object(env, &out));
+  NAPI_OK(napi_set_named_property(env, out, "index", idx));
+  NAPI_OK(napi_set_named_property(env, out, "t", t));
+  return out;
+}
 napi_value Stats(napi_env env, napi_callback_info info) {
   napi_value a[1];
   if (!args(env, info, 1, a)) return nullptr;
@@ -409,6 +428,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"readAccum", 0, ReadAccum, 0, 0, 0, napi_enumerable, 0},
       {"filter", 0, Filter, 0, 0, 0, napi_enumerable, 0},
       {"stats", 0, Stats, 0, 0, 0, napi_enumerable, 0},
+      {"pick", 0, Pick, 0, 0, 0, napi_enumerable, 0},
       {"camera", 0, Camera, 0, 0, 0, napi_enumerable, 0},
       {"jitterInverse", 0, JitterInverse, 0, 0, 0, napi_enumerable, 0},
       {"schedule", 0, Schedule, 0, 0, 0, napi_enumerable, 0},

@@ -51,6 +51,8 @@ class Renderer {
   }
 
   update(scene) {
+    // the picker (Control / Pickup) finds the renderer that holds this scene on the device
+    Object.defineProperty(scene, 'renderer', { value: this, writable: true, configurable: true, enumerable: false });
     this.filter = filterConfig(scene.rendererConfig().filter);
     const s = scene.serialize();
     this.lib.setScene(this.ctx, s.objects, s.n, s.texparams, s.tn, s.lights, s.ln, masksOf(scene.tracerConfig()));
@@ -117,6 +119,15 @@ class Renderer {
     }
     return this.pixels;
   }
+
+  // Pickup.pick on the GPU: the trace kernel's primitive sweep for one ray -> {index (object row, -1 = miss), t}
+  pick(origin, dir) {
+    const rays = Float32Array.from([...origin, ...dir]);
+    const r = this.lib.pick(this.ctx, rays);
+    return { index: r.index[0], t: r.t[0] };
+  }
+  // many rays at once: Float32Array of 6 floats per ray -> {index: Int32Array, t: Float32Array}
+  pickRays(rays) { return this.lib.pick(this.ctx, rays); }
 
   readPixels() { return this.lib.readback(this.ctx, false).rgba; }
   readAccum() { return this.lib.readAccum(this.ctx); }

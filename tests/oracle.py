@@ -41,6 +41,8 @@ def lib(count: bool = False) -> ctypes.CDLL:
     L.oracle_filter.argtypes = [f32p, ci, ci, ci, f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p]
     L.oracle_filter_aov.restype = ci
     L.oracle_filter_aov.argtypes = [f32p, f32p, f32p, ci, ci, ci, ctypes.c_float, ctypes.c_float, f32p]
+    L.oracle_pick.restype = ci
+    L.oracle_pick.argtypes = [f32p, ci, f32p, ci, u32, f32p, ci, ctypes.POINTER(ctypes.c_int), f32p]
     L.oracle_math.restype = None
     L.oracle_math.argtypes = [ci, f32p, f32p, f32p, ci]
     L.oracle_intersect_t.restype = ctypes.c_float
@@ -104,6 +106,19 @@ def filter_aov(mean: np.ndarray, normal: np.ndarray, position: np.ndarray, kind:
     if rc:
         raise RuntimeError(f"oracle_filter_aov: {rc}")
     return out
+
+
+def pick(sc: dict, shape_mask: int, rays) -> tuple:
+    """the shader's intersectObjects for (count, 6) rays -> (object row or -1, distance)"""
+    L = lib()
+    r = _f(rays).reshape(-1, 6)
+    idx = np.zeros(len(r), dtype=np.int32)
+    t = np.zeros(len(r), dtype=np.float32)
+    rc = L.oracle_pick(_p(_f(sc["objects"])), sc["n"], _p(_f(sc["texparams"])), sc["tn"], shape_mask, _p(r), len(r),
+                       idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _p(t))
+    if rc:
+        raise RuntimeError(f"oracle_pick: {rc}")
+    return idx, t
 
 
 def math(fn: int, x, y=None) -> np.ndarray:

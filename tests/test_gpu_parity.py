@@ -257,3 +257,34 @@ def test_aov_filter_needs_aov_flag(gpu, fixtures):
     with pytest.raises(RuntimeError):
         ctx.filter(capi.FILTER_WAVELET, None, 2.0, 2.0)
     ctx.close()
+
+
+# ---- picking: sail_pick (GPU) vs the oracle's intersectObjects -------------------------------------------------
+def _pick_rays(sc, W, H, count, rng):
+    """camera rays through random pixels (Ray.generate, pickup.js:11-14: inverse(P*MV) * (x, y, 0, 1) / w - eye,
+    not normalised) plus rays from random interior points in random directions"""
+    mvp = np.array(sc["mvp_rowmajor"])
+    inv = np.linalg.inv(mvp)
+    eye = np.array(sc["eye"], dtype=np.float64)
+    xs = rng.uniform(-1, 1, count // 2)
+    ys = rng.uniform(-1, 1, count // 2)
+    p = inv @ np.stack([xs, ys, np.zeros_like(xs), np.ones_like(xs)])
+    d = (p[:3] / p[3]).T - eye
+    cam = np.concatenate([np.tile(eye, (len(d), 1)), d], axis=1)
+    o = rng.uniform(0.5, 5.0, (count - len(d), 3))
+    dd = rng.normal(size=(count - len(d), 3))
+    return np.concatenate([cam, np.concatenate([o, dd], axis=1)]).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "ALL", "UI"])
+def test_pick_matches_oracle(gpu, fixtures, name):
+    sc = fixtures["scenes"][name]
+    rays = _pick_rays(sc, 64, 64, 4096, np.random.default_rng(5))
+    ctx = capi.Context(16, 16)
+    ctx.set_scene_dict(sc)
+    idx, t = ctx.pick(rays)
+    ctx.close()
+    widx, wt = oracle.pick(sc, capi.plugin_masks(sc["plugins"])[0], rays)
+    assert np.array_equal(idx, widx)
+    assert np.array_equal(t.view(np.uint32), wt.view(np.uint32))
+    assert (idx >= 0).mean() > 0.5

@@ -117,3 +117,22 @@ def test_js_aov_display_filters(tmp_path, flt, r, kind):
     want = oracle.filter_aov(rd["mean"], rd["normal"], rd["position"], kind, rx, ry)
     want8 = np.floor(np.clip(want[..., :3], 0, 1) * 255.0 + 0.5).astype(np.uint8)
     assert (rgba8[..., :3] == want8).all()
+
+
+@pytest.mark.gpu
+def test_js_pick_and_drag(tmp_path, exported):
+    """Sail.Control / Pickup: clicks are answered on the GPU by the trace kernel's sweep (sail_pick) and match
+    the oracle's intersectObjects for the same rays; a drag moves the sphere and restarts accumulation"""
+    if capi.device_count() < 1:
+        pytest.skip("no HIP device")
+    out = str(tmp_path / "pick.json")
+    subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "pick_check.js"), out], cwd=ROOT, check=True, timeout=300)
+    with open(out) as f:
+        res = json.load(f)
+    sc = exported["C1"]
+    idx, _ = oracle.pick(sc, capi.plugin_masks(sc["plugins"])[0], np.array(res["rays"], dtype=np.float32))
+    assert list(idx) == res["picked"]
+    assert set(res["picked"]) >= {1, 2}
+    assert res["selected"] == 2 and res["began"]
+    assert res["after"][0] != res["before"][0] and res["after"][1] == pytest.approx(res["before"][1])
+    assert res["sampleCount"] == 2  # the drag frame restarted at k = 0, then one more frame
