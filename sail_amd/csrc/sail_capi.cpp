@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <math.h>
+#include <cmath>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -105,6 +106,7 @@ struct sail_ctx {
   sail_plugins plugins{};
   bool haveScene = false;
   int shadowAnyHit = 0;
+  int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
   int launchSpp = 32;
@@ -246,6 +248,68 @@ void quadricHost(SailPrim& p) {
   if (p.type == SAIL_PARABOLOID) p.a[6] = hwmax(p.a[3], p.a[4]) / (p.a[5] * p.a[5]);
 }
 
+// Conservative world-space bounds of what each primitive's intersection can return, padded, in a[18..23]
+// (min xyz, max xyz; +-inf when the shape has no finite bound). The trace kernel uses them for a cheap f32
+// pre-cull before the exact per-primitive test: a primitive whose padded box the ray misses, or enters
+// beyond the closest distance so far, cannot change the sweep's result (n = 67).
+// Local frames: OBJECT_SPACE maps world (x, y, z) -> local (-z, x, y), so the local z axis is world y.
+void primBoundsHost(SailPrim& p) {
+  const double inf = INFINITY;
+  double lo[3] = {-inf, -inf, -inf}, hi[3] = {inf, inf, inf};
+  const float* a = p.a;
+  auto box = [&](double x0, double y0, double z0, double x1, double y1, double z1) {
+    lo[0] = fmin(x0, x1); lo[1] = fmin(y0, y1); lo[2] = fmin(z0, z1);
+    hi[0] = fmax(x0, x1); hi[1] = fmax(y0, y1); hi[2] = fmax(z0, z1);
+  };
+  switch (p.type) {
+    case SAIL_CUBE: case SAIL_CORNELLBOX: box(a[0], a[1], a[2], a[3], a[4], a[5]); break;
+    case SAIL_RECTANGLE: {  // corners mn + {0, maxX} ss + {0, maxY} ts (rectangle.glsl:32-63)
+      const double ss[3] = {a[9], a[10], a[11]}, ts[3] = {a[12], a[13], a[14]}, mx = a[15], my = a[16];
+      for (int k = 0; k < 3; k++) {
+        const double c0 = a[k], c1 = a[k] + mx * ss[k], c2 = a[k] + my * ts[k], c3 = a[k] + mx * ss[k] + my * ts[k];
+        lo[k] = fmin(fmin(c0, c1), fmin(c2, c3));
+        hi[k] = fmax(fmax(c0, c1), fmax(c2, c3));
+      }
+      break;
+    }
+    case SAIL_SPHERE: { const double r = fabs(a[3]); box(a[0] - r, a[1] - r, a[2] - r, a[0] + r, a[1] + r, a[2] + r); break; }
+    case SAIL_CONE: case SAIL_CYLINDER: {  // radius <= rad for local z in [-EPS, h]
+      const double r = fabs(a[4]);
+      box(a[0] - r, a[1], a[2] - r, a[0] + r, a[1] + a[3], a[2] + r);
+      break;
+    }
+    case SAIL_DISK: { const double r = fabs(a[3]); box(a[0] - r, a[1], a[2] - r, a[0] + r, a[1], a[2] + r); break; }
+    case SAIL_HYPERBOLOID: {  // ah (x^2 + y^2) - ch z^2 = 1 for z in [zMin, zMax] (a[12], a[13])
+      const double ah = a[9], ch = a[10], z0 = a[12], z1 = a[13];
+      double r2 = -1.0;
+      if (ah > 0.0 && z0 <= z1) {
+        const double zs[3] = {z0, z1, (z0 < 0.0 && z1 > 0.0) ? 0.0 : z0};
+        for (double z : zs) r2 = fmax(r2, (1.0 + ch * z * z) / ah);
+      }
+      if (r2 >= 0.0 && std::isfinite(r2)) {
+        const double r = sqrt(r2);
+        box(a[0] - r, a[1] + z0, a[2] - r, a[0] + r, a[1] + z1, a[2] + r);
+      }
+      break;
+    }
+    case SAIL_PARABOLOID: {  // k (x^2 + y^2) = z, k = zMax / rad^2 (a[6]); z in [min(z0,z1), max(z0,z1)]
+      const double k = a[6], z0 = fmin(a[3], a[4]), z1 = fmax(a[3], a[4]);
+      if (k > 0.0 && std::isfinite(k) && z1 >= 0.0) {
+        const double r = sqrt(z1 / k);
+        box(a[0] - r, a[1] + z0, a[2] - r, a[0] + r, a[1] + z1, a[2] + r);
+      }
+      break;
+    }
+    default: break;
+  }
+  for (int k = 0; k < 3; k++) {
+    if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) { lo[k] = -inf; hi[k] = inf; continue; }
+    const double pad = 1e-3 + 1e-4 * fmax(fabs(lo[k]), fabs(hi[k]));
+    lo[k] -= pad; hi[k] += pad;
+  }
+  for (int k = 0; k < 3; k++) { p.a[18 + k] = (float)lo[k]; p.a[21 + k] = (float)hi[k]; }
+}
+
 void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk) {
   TexView o{objects, 18, n};
   const float L = 17.0f;
@@ -305,6 +369,7 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
     }
     p.em[0] = v3[0]; p.em[1] = v3[1]; p.em[2] = v3[2];
     quadricHost(p);
+    primBoundsHost(p);
     // only slabs return t > EPSILON strictly; anything else may tie or undercut EPSILON, so shadow
     // rays must then find the true closest distance (shader.light.js:24-31)
     if (cat != SAIL_CUBE && cat != SAIL_CORNELLBOX) *anyHitOk = 0;
@@ -346,6 +411,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.rank = (c->partMode == SAIL_PART_SAMPLES) ? 0 : c->rank;
     A.ownedTiles = owned;
     A.shadowAnyHit = c->shadowAnyHit;
+    A.cullPrims = c->n >= c->cullMinPrims;
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     hipEvent_t e0, e1;
     if ((rc = getEvent(c, &e0)) || (rc = getEvent(c, &e1))) return rc;
@@ -385,6 +451,7 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
   if (device >= ndev) return fail(nullptr, SAIL_E_INVALID, "device %d out of range (%d devices)", device, ndev);
   sail_ctx* c = new sail_ctx();
   c->device = device; c->W = width; c->H = height; c->flags = flags;
+  if (const char* e = getenv("SAIL_CULL_MIN_PRIMS")) c->cullMinPrims = atoi(e);  // tests force the pre-cull on/off
   auto bail = [&](int code, const char* what) {
     g_create_error = std::string("sail_create: ") + what;
     sail_destroy(c);

@@ -25,7 +25,7 @@ struct __attribute__((aligned(16))) SailPrim {
   int32_t texRow;   // texParams row of the texture
   float em[3];      // emission (Cornellbox: forced BLACK, cornellbox.glsl:19)
   float pad0;
-  float a[24];      // shape parameters in row order (see sail_scene.cpp decode)
+  float a[24];      // shape parameters in row order, per-scene constants, a[18..23] padded bounds (sail_capi.cpp)
 };
 
 // Per-sample uniforms (the reference's per-frame `matrix` + `timeSinceStart` + `textureWeight`,
@@ -59,6 +59,7 @@ struct SailTraceArgs {
   int world, rank;          // tile partition: global tile t belongs to rank t % world
   int ownedTiles;           // tiles of this rank
   int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
+  int cullPrims;            // 1: padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test
 };
 
 struct SailFilterArgs {

@@ -156,6 +156,7 @@ struct Ctx {
   uint32_t matMask, texMask, lightMask;
   float fcx, fcy;
   int shadowAnyHit;
+  int cullPrims;
 };
 
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
@@ -561,10 +562,24 @@ D float primT(const SailPrim& p, const Ray& r, V3* hl) {
   }
 }
 
+// Cheap conservative pre-cull: the ray against the primitive's padded bounds in f32 (sail_capi.cpp
+// primBoundsHost). It rejects only rays that miss the padded box or enter it beyond the closest distance so
+// far (with margin); such a primitive's exact test could only return a miss or a larger distance.
+D bool padHit(const SailPrim& p, const Ray& r, float best) {
+  const float ix = (float)r.rx, iy = (float)r.ry, iz = (float)r.rz;
+  const float x0 = (p.a[18] - r.o.x) * ix, x1 = (p.a[21] - r.o.x) * ix;
+  const float y0 = (p.a[19] - r.o.y) * iy, y1 = (p.a[22] - r.o.y) * iy;
+  const float z0 = (p.a[20] - r.o.z) * iz, z1 = (p.a[23] - r.o.z) * iz;
+  const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
+  const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
+  return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > best * 1.0001f + 1e-4f);
+}
+
 // closest distance only (shadow rays, testShadow shader.light.js:24-31)
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   for (int i = 0; i < c.n; i++) {
+    if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
     const float t = primT(c.prims[i], r, nullptr);
     if (t < best) {
       best = t;
@@ -582,6 +597,7 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   V3 bhl = v3s(0.0f);
 #if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
+    if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
     V3 hl = v3s(0.0f);
     const float t = primT(c.prims[i], r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
@@ -991,7 +1007,9 @@ D float q8(float v) {
 #ifndef SAIL_TRACE_MIN_WAVES
 #define SAIL_TRACE_MIN_WAVES 6
 #endif
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
+// CULL selects the padded-box pre-cull at compile time (two kernels), so small scenes carry none of its code.
+template <bool CULL>
+__device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   const int ownedTile = blockIdx.x >> 4;
   const int sub = blockIdx.x & 15;
   const int tile = A.rank + ownedTile * A.world;
@@ -1023,6 +1041,7 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_tra
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
   c.shadowAnyHit = A.shadowAnyHit;
+  c.cullPrims = CULL ? 1 : 0;
 
   const size_t pix = (size_t)y * A.W + x;
   float4 acc = A.accum[pix];
@@ -1062,6 +1081,12 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_tra
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
     if (lane == 0) atomicAdd(A.segCounter, v);
   }
+}
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
+  traceTile<false>(A);
+}
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
+  traceTile<true>(A);
 }
 
 // ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
@@ -1226,7 +1251,8 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
 
 // ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
+  if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
+  else hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
   return hipGetLastError();
 }
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s) {

@@ -288,3 +288,14 @@ def test_pick_matches_oracle(gpu, fixtures, name):
     assert np.array_equal(idx, widx)
     assert np.array_equal(t.view(np.uint32), wt.view(np.uint32))
     assert (idx >= 0).mean() > 0.5
+
+
+# ---- the padded-box pre-cull (scenes with >= 8 primitives) must not change a single bit -----------------------
+@pytest.mark.parametrize("name,W,H,spp,B", [("C1", 48, 32, 4, 5), ("C3", 40, 40, 3, 8), ("ALL", 40, 32, 3, 6),
+                                            ("UI", 32, 32, 3, 5)])
+@pytest.mark.parametrize("cull", ["0", "1000"])
+def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, B, cull):
+    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)   # 0: cull every scene, 1000: never
+    got, want, st, segs, _, _ = _render_both(fixtures, name, W, H, spp, B, launch=2)
+    assert bit_equal(got, want).all()
+    assert st.segments == segs
