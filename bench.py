@@ -28,10 +28,10 @@ from sail_amd import capi  # noqa: E402
 
 # BASELINE.json configs: [1] is the headline (default); the others are selectable with --config for study
 CONFIGS = {
-    "C2": {"workload": "cornell_box_readme_C2", "scene": "C1", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
-    "C3": {"workload": "materials_demo_C3", "scene": "C3", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
-    "C4": {"workload": "random64_C4", "scene": "C4", "width": 3840, "height": 2160, "bounces": 12, "spp": 256},
-    "C5": {"workload": "cornell_box_converged_C5", "scene": "C1", "width": 1920, "height": 1080, "bounces": 16, "spp": 65536},
+    "C2": {"workload": "cornell_box_readme_C2", "desc": "README Cornell box", "scene": "C1", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
+    "C3": {"workload": "materials_demo_C3", "desc": "materials demo", "scene": "C3", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
+    "C4": {"workload": "random64_C4", "desc": "random-64 primitives", "scene": "C4", "width": 3840, "height": 2160, "bounces": 12, "spp": 256},
+    "C5": {"workload": "cornell_box_converged_C5", "desc": "README Cornell box (converged)", "scene": "C1", "width": 1920, "height": 1080, "bounces": 16, "spp": 65536},
 }
 CONFIG = CONFIGS["C2"]
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
@@ -87,15 +87,15 @@ def ops_per_segment(sc, masks, mvp, W, H, B):
     return ops / max(segs, 1)
 
 
-def profiled_traffic(px, spp, bounces):
-    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same launch shape
-    (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary.json); None if none matches."""
+def profiled_traffic(workload, px, spp, bounces):
+    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same workload and
+    launch shape (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary*.json); None if none matches."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
         L = rec.get("launch", {})
-        if L.get("pixels") == px and L.get("spp") == spp and L.get("bounces") == bounces:
+        if rec.get("workload", "cornell_box_readme_C2") == workload and L.get("pixels") == px and L.get("spp") == spp and L.get("bounces") == bounces:
             return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -191,7 +191,7 @@ def main():
         ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
-        traffic, traffic_src = profiled_traffic(tiles_px, args.launch_spp, B)
+        traffic, traffic_src = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B)
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
@@ -205,7 +205,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: frozen README Cornell box rows (reference serializer), deterministic sample schedule",
+            "data": f"synthetic: frozen {cfg['desc']} scene rows (SURVEY §8(d), JS API == reference serializer), "
+                    "deterministic sample schedule",
             "config": {"workload": cfg["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
                        "launch_spp": args.launch_spp, "partition": f"tiles64x{world}", "segments_per_step": W * H * spp * B},
             "roofline": {

@@ -916,6 +916,10 @@ D bool testShadow(const Ctx& c, const Ray& r) {
   const float d = closestT(c, r);
   return d > kEps && d < kOneMinusEps;
 }
+// The light categories only differ in how they build the shadow ray and the unoccluded contribution; the
+// shadow sweep itself (the expensive part) is shared, so a wave whose lanes picked different light kinds
+// runs one sweep instead of one per kind. Contribution and visibility are independent pure functions of the
+// same inputs, so evaluating the contribution first changes no bit.
 D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   // randomInt(seed,0,ln) = int(random2(seed).x * ln): the same hash as the BSDF sample's first component
   const int index = to_int(u2.x * (float)c.ln);
@@ -925,28 +929,26 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   if (cat < 0 || cat >= 32 || !((c.lightMask >> cat) & 1u)) return v3s(0.0f);
   const int row = (c.ln == 1) ? 0 : (index < 0 ? 0 : (index > c.ln - 1 ? c.ln - 1 : index));
   const float* L = c.lt + row * 18;
-  if (cat == SAIL_AREA) {
+  V3 contrib = v3s(0.0f), toLight = v3s(0.0f);
+  bool lit = false;
+  if (cat == SAIL_AREA) {  // light/area.glsl
     const V3 em = v3(L[2], L[3], L[4]);
     V3 normal; float pdf;
     const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
-    const V3 toLight = p - ins.hit;
+    toLight = p - ins.hit;
     const V3 nt = normalize(toLight);
-    const Ray sr = mkRay(ins.hit, toLight);
-    if (testShadow(c, sr)) return v3s(0.0f);
-    return em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
-  } else if (cat == SAIL_POINT) {
+    contrib = em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
+    lit = true;
+  } else if (cat == SAIL_POINT) {  // light/point.glsl:13-20
     const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
     const V3 p = from + uniformSampleSphere(u2) * 0.1f;
-    const V3 toLight = p - ins.hit;
-    const Ray sr = mkRay(ins.hit, toLight);
-    if (testShadow(c, sr)) return v3s(0.0f);
-    return em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
-  } else if (cat == SAIL_SPOT) {
+    toLight = p - ins.hit;
+    contrib = em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
+    lit = true;
+  } else if (cat == SAIL_SPOT) {  // light/spot.glsl
     const float ctw = L[1], cfs = L[2];
     const V3 from = v3(L[3], L[4], L[5]), em = v3(L[6], L[7], L[8]);
-    const V3 toLight = from - ins.hit;
-    const Ray sr = mkRay(ins.hit, toLight);
-    if (testShadow(c, sr)) return v3s(0.0f);
+    toLight = from - ins.hit;
     const V3 nt = normalize(toLight);
     const float d = length(toLight);
     float fall;
@@ -956,9 +958,13 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
       else if (cT >= cfs) fall = 1.0f;
       else { const float delta = (cT - ctw) / (cfs - ctw); const float d2 = delta * delta; fall = d2 * d2; }
     }
-    return em * fall * fmax_(0.0f, dot(normalize(toLight), ins.normal)) / (d * d);
+    contrib = em * fall * fmax_(0.0f, dot(normalize(toLight), ins.normal)) / (d * d);
+    lit = true;
   }
-  return v3s(0.0f);
+  if (!lit) return v3s(0.0f);
+  // testShadow(Ray(hit, toLight)) (shader.light.js:24-31): unnormalised direction, no origin offset
+  if (testShadow(c, mkRay(ins.hit, toLight))) return v3s(0.0f);
+  return contrib;
 }
 
 // ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
@@ -1085,7 +1091,11 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
   traceTile<false>(A);
 }
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
+// the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
+#ifndef SAIL_TRACE_CULL_MIN_WAVES
+#define SAIL_TRACE_CULL_MIN_WAVES 8
+#endif
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CULL_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
   traceTile<true>(A);
 }
 

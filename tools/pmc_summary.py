@@ -4,7 +4,8 @@
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports
 half of the bytes of a wide (16 B/lane) coalesced streaming read, which is this kernel's accumulator read,
 so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.
-Usage: tools/pmc_summary.py gpurun_out/pmc out.json [launch_pixels launch_spp bounces]
+Usage: tools/pmc_summary.py gpurun_out/pmc out.json [launch_pixels launch_spp bounces [workload]]
+Counters are summed over the chip (all XCDs) per dispatch; each value here is the mean over dispatches.
 """
 import collections
 import csv
@@ -28,6 +29,7 @@ def main():
     px = int(sys.argv[3]) if len(sys.argv) > 3 else 1920 * 1080
     spp = int(sys.argv[4]) if len(sys.argv) > 4 else 32
     bounces = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+    workload = sys.argv[6] if len(sys.argv) > 6 else "cornell_box_readme_C2"
     c = {}
     for p in ("fetch", "write", "sq", "sq2"):
         if os.path.isdir(os.path.join(pdir, p)):
@@ -38,7 +40,7 @@ def main():
     waves = c.get("SQ_WAVES", 0)
     segs = px * spp * bounces
     rec = {
-        "kernel": "sail_trace_kernel", "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
+        "kernel": "sail_trace_kernel", "workload": workload, "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
         "hbm": {"fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
                 "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,
                 "raw_FETCH_SIZE_KiB": c["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": c["WRITE_SIZE"]},
@@ -49,6 +51,9 @@ def main():
             "valu_insts_per_wave": c["SQ_INSTS_VALU"] / waves,
             "valu_insts_per_segment_lane": c["SQ_INSTS_VALU"] * 64 / segs,
             "salu_insts_per_wave": c.get("SQ_INSTS_SALU", 0) / waves,
+            # beyond the one float4 accumulator store per lane: scratch (register spill) stores
+            "vmem_writes_per_wave": c.get("SQ_INSTS_VMEM_WR", 0) / waves,
+            "vmem_reads_per_segment_lane": c.get("SQ_INSTS_VMEM_RD", 0) * 64 / segs,
         }
         if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
             # lanes doing work per VALU cycle; 1.0 = no divergence or masked lanes
