@@ -107,6 +107,7 @@ struct sail_ctx {
   bool haveScene = false;
   int shadowAnyHit = 0;
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
+  int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
   int launchSpp = 32;
@@ -139,6 +140,17 @@ int fail(sail_ctx* c, int code, const char* fmt, ...) {
     hipError_t e_ = (call);                                                                        \
     if (e_ != hipSuccess) return fail((ctx), SAIL_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
   } while (0)
+
+// the smallest precompiled plugin-set kernel that covers the scene (sail_device.h SAIL_KSET_*)
+int kernelSetFor(const sail_ctx* c) {
+  if (c->forceGeneric || c->n >= c->cullMinPrims) return SAIL_KSET_GENERIC;
+  const sail_plugins& p = c->plugins;
+  const bool lightsOk = c->ln == 0 || (p.light_mask & ~SAIL_KSET_CORNELL_LIGHTS) == 0;
+  if ((p.shape_mask & ~SAIL_KSET_CORNELL_SHAPES) == 0 && (p.material_mask & ~SAIL_KSET_CORNELL_MATS) == 0 &&
+      (p.texture_mask & ~SAIL_KSET_CORNELL_TEX) == 0 && lightsOk && SAIL_KSET_CORNELL_LIGHTS == 0 && c->ln == 0)
+    return SAIL_KSET_CORNELL;
+  return SAIL_KSET_GENERIC;
+}
 
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
   const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
@@ -412,6 +424,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.ownedTiles = owned;
     A.shadowAnyHit = c->shadowAnyHit;
     A.cullPrims = c->n >= c->cullMinPrims;
+    A.kernelSet = kernelSetFor(c);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     hipEvent_t e0, e1;
     if ((rc = getEvent(c, &e0)) || (rc = getEvent(c, &e1))) return rc;
@@ -452,6 +465,7 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
   sail_ctx* c = new sail_ctx();
   c->device = device; c->W = width; c->H = height; c->flags = flags;
   if (const char* e = getenv("SAIL_CULL_MIN_PRIMS")) c->cullMinPrims = atoi(e);  // tests force the pre-cull on/off
+  if (const char* e = getenv("SAIL_FORCE_GENERIC")) c->forceGeneric = atoi(e);
   auto bail = [&](int code, const char* what) {
     g_create_error = std::string("sail_create: ") + what;
     sail_destroy(c);

@@ -60,7 +60,16 @@ struct SailTraceArgs {
   int ownedTiles;           // tiles of this rank
   int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
   int cullPrims;            // 1: padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test
+  int kernelSet;            // SAIL_KSET_*: the precompiled plugin-set kernel to launch
 };
+
+// Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a
+// set's masks may use that set's kernel; everything else runs the generic one.
+enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1 };
+#define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))
+#define SAIL_KSET_CORNELL_MATS ((1u << SAIL_MATTE) | (1u << SAIL_MIRROR))
+#define SAIL_KSET_CORNELL_TEX 0u
+#define SAIL_KSET_CORNELL_LIGHTS 0u
 
 struct SailFilterArgs {
   const float4* accum;

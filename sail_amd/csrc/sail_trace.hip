@@ -157,7 +157,12 @@ struct Ctx {
   float fcx, fcy;
   int shadowAnyHit;
   int cullPrims;
+  // plugin sets compiled into this kernel instantiation (compile-time constants after inlining): the
+  // reference generates one GLSL program per scene plugin set (shader.js combinefs); this build precompiles
+  // kernels for plugin subsets and dispatches the smallest one that covers the scene
+  uint32_t kShapes, kMats, kTex, kLights;
 };
+#define HAS(set, id) (((set) >> (id)) & 1u)
 
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
 D float TP(const Ctx& c, int row, int col) { return c.tp[row * 16 + col]; }
@@ -204,31 +209,32 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
   if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
   if (cat < 0 || cat >= 32 || !((c.texMask >> cat) & 1u)) return v3s(0.0f);
   switch (cat) {
-    case SAIL_TEX_CHECKERBOARD: {
+    case SAIL_TEX_CHECKERBOARD: if (!HAS(c.kTex, SAIL_TEX_CHECKERBOARD)) break; {
       const float size = TP(c, texRow, 1), lineWidth = TP(c, texRow, 2);
       const float width = 0.5f * lineWidth / size;
       const float fx = uv.x / size - floorf(uv.x / size), fy = uv.y / size - floorf(uv.y / size);
       const bool in_outline = (fx < width || fx > 1.0f - width) || (fy < width || fy > 1.0f - width);
       return in_outline ? v3s(0.5f) : v3s(1.0f);
     }
-    case SAIL_TEX_CHECKERBOARD2: {
+    case SAIL_TEX_CHECKERBOARD2: if (!HAS(c.kTex, SAIL_TEX_CHECKERBOARD2)) break; {
       const float size = TP(c, texRow, 7);
       const float qx = floorf(uv.x / size), qy = floorf(uv.y / size);
       return (to_int(qx + qy) % 2 == 0) ? TP3(c, texRow, 1) : TP3(c, texRow, 4);
     }
-    case SAIL_TEX_BILERP: {
+    case SAIL_TEX_BILERP: if (!HAS(c.kTex, SAIL_TEX_BILERP)) break; {
       const V3 c00 = TP3(c, texRow, 1), c01 = TP3(c, texRow, 4), c10 = TP3(c, texRow, 7), c11 = TP3(c, texRow, 10);
       return (1.0f - uv.x) * (1.0f - uv.y) * c00 + (1.0f - uv.x) * (uv.y) * c01 + (uv.x) * (1.0f - uv.y) * c10 +
              (uv.x) * (uv.y) * c11;
     }
-    case SAIL_TEX_MIXF: {
+    case SAIL_TEX_MIXF: if (!HAS(c.kTex, SAIL_TEX_MIXF)) break; {
       const float amount = TP(c, texRow, 7);
       return (1.0f - amount) * TP3(c, texRow, 1) + amount * TP3(c, texRow, 4);
     }
-    case SAIL_TEX_SCALE: return TP3(c, texRow, 1) * TP3(c, texRow, 4);
-    case SAIL_TEX_UVF: return v3(uv.x - floorf(uv.x), uv.y - floorf(uv.y), 0.0f);
-    default: return v3s(0.0f);
+    case SAIL_TEX_SCALE: if (!HAS(c.kTex, SAIL_TEX_SCALE)) break; return TP3(c, texRow, 1) * TP3(c, texRow, 4);
+    case SAIL_TEX_UVF: if (!HAS(c.kTex, SAIL_TEX_UVF)) break; return v3(uv.x - floorf(uv.x), uv.y - floorf(uv.y), 0.0f);
+    default: break;
   }
+  return v3s(0.0f);
 }
 
 // ---- slab boxes: cube.glsl:65-87, cornellbox.glsl:67-90, boundbox.glsl:6-17 ------------------------------
@@ -547,19 +553,20 @@ D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
 }
 
 // hl (may be null): the local-space hit point of the shapes whose hit record starts from it
-D float primT(const SailPrim& p, const Ray& r, V3* hl) {
+D float primT(const Ctx& c, const SailPrim& p, const Ray& r, V3* hl) {
   switch (p.type) {
-    case SAIL_CUBE: return cubeT(p, r);
-    case SAIL_SPHERE: return sphereT(p, r, hl);
-    case SAIL_RECTANGLE: return rectT(p, r, hl);
-    case SAIL_CONE: return coneT(p, r, hl);
-    case SAIL_CYLINDER: return cylinderT(p, r, hl);
-    case SAIL_DISK: return diskT(p, r, hl);
-    case SAIL_HYPERBOLOID: return hypT(p, r, hl);
-    case SAIL_PARABOLOID: return paraT(p, r, hl);
-    case SAIL_CORNELLBOX: return cornellT(p, r);
-    default: return kMaxDistance;
+    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) return cubeT(p, r); break;
+    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) return sphereT(p, r, hl); break;
+    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) return rectT(p, r, hl); break;
+    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) return coneT(p, r, hl); break;
+    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) return cylinderT(p, r, hl); break;
+    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) return diskT(p, r, hl); break;
+    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) return hypT(p, r, hl); break;
+    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) return paraT(p, r, hl); break;
+    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) return cornellT(p, r); break;
+    default: break;
   }
+  return kMaxDistance;
 }
 
 // Cheap conservative pre-cull: the ray against the primitive's padded bounds in f32 (sail_capi.cpp
@@ -580,7 +587,7 @@ D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   for (int i = 0; i < c.n; i++) {
     if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
-    const float t = primT(c.prims[i], r, nullptr);
+    const float t = primT(c, c.prims[i], r, nullptr);
     if (t < best) {
       best = t;
       if (c.shadowAnyHit && best > kEps && best < kOneMinusEps) break;  // exact: no prim returns t <= EPSILON
@@ -599,15 +606,15 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   for (int i = 0; i < c.n; i++) {
     if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
     V3 hl = v3s(0.0f);
-    const float t = primT(c.prims[i], r, &hl);
+    const float t = primT(c, c.prims[i], r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
   }
 #else
   for (int i = 0; i < c.n; i++) {
-    const float t = primT(c.prims[i], r, nullptr);
+    const float t = primT(c, c.prims[i], r, nullptr);
     if (t < best) { best = t; bi = i; }
   }
-  if (bi >= 0) primT(c.prims[bi], r, &bhl);  // the same arithmetic again, for the winner only
+  if (bi >= 0) primT(c, c.prims[bi], r, &bhl);  // the same arithmetic again, for the winner only
 #endif
   Hit h;
   h.d = best;
@@ -616,15 +623,15 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   if (bi < 0) return h;
   const SailPrim& p = c.prims[bi];
   switch (p.type) {
-    case SAIL_CUBE: cubeHit(c, p, r, best, h); break;
-    case SAIL_SPHERE: sphereHit(c, p, bhl, h); break;
-    case SAIL_RECTANGLE: rectHit(c, p, bhl, h); break;
-    case SAIL_CONE: coneHit(c, p, bhl, h); break;
-    case SAIL_CYLINDER: cylinderHit(c, p, bhl, h); break;
-    case SAIL_DISK: diskHit(c, p, bhl, h); break;
-    case SAIL_HYPERBOLOID: hypHit(c, p, bhl, h); break;
-    case SAIL_PARABOLOID: paraHit(c, p, bhl, h); break;
-    case SAIL_CORNELLBOX: cornellHit(p, r, best, h); break;
+    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) cubeHit(c, p, r, best, h); break;
+    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) sphereHit(c, p, bhl, h); break;
+    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) rectHit(c, p, bhl, h); break;
+    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) coneHit(c, p, bhl, h); break;
+    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) cylinderHit(c, p, bhl, h); break;
+    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) diskHit(c, p, bhl, h); break;
+    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) hypHit(c, p, bhl, h); break;
+    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) paraHit(c, p, bhl, h); break;
+    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) cornellHit(p, r, best, h); break;
     default: break;
   }
   h.matRow = p.matRow;
@@ -644,7 +651,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
   const SailPrim& p = c.prims[row];
   const float s = sgn(p.rev);
   switch (p.type) {
-    case SAIL_SPHERE: {
+    case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
       const V3 q = uniformSampleSphere(u);
       const float rad = p.a[3];
       pdf = kInvPI / (rad * rad);
@@ -652,7 +659,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       normal = s * (res - P3(p, 0)) / rad;
       return res;
     }
-    case SAIL_RECTANGLE: {
+    case SAIL_RECTANGLE: if (!HAS(c.kShapes, SAIL_RECTANGLE)) break; {
       const V3 mn = P3(p, 0), mx = P3(p, 3);
       const V3 x = v3(mx.x - mn.x, 0.0f, 0.0f), y = v3(0.0f, mx.y - mn.y, mx.z - mn.z);
       pdf = p.a[17];                                   // 1 / (length(x) * length(y)), per scene
@@ -660,7 +667,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       normal = s * P3(p, 6);                           // normalize(cross(x, y)) == the frame normal
       return res;
     }
-    case SAIL_DISK: {
+    case SAIL_DISK: if (!HAS(c.kShapes, SAIL_DISK)) break; {
       const V2 pd = concentricSampleDisk(u);
       const V3 pp = P3(p, 0);
       const float rad = p.a[3], ri = p.a[4];
@@ -670,8 +677,8 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       normal = s * v3(0.0f, 1.0f, 0.0f);
       return res;
     }
-    case SAIL_CUBE: normal = normalForCube(v3s(0.0f), p); return v3s(0.0f);
-    case SAIL_CORNELLBOX: normal = normalForCornellbox(v3s(0.0f), p); return v3s(0.0f);
+    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) normal = normalForCube(v3s(0.0f), p); return v3s(0.0f);
+    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) normal = normalForCornellbox(v3s(0.0f), p); return v3s(0.0f);
     case SAIL_CONE: {  // cone.glsl:38-46 at BLACK
       const V3 hit = v3s(0.0f) - P3(p, 0);
       const float h = p.a[3], rad = p.a[4];
@@ -681,12 +688,12 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       normal = s * normalize(hit - v3(0.0f, 0.0f, h - x1 - x2));
       return v3s(0.0f);
     }
-    case SAIL_CYLINDER: {
+    case SAIL_CYLINDER: if (!HAS(c.kShapes, SAIL_CYLINDER)) break; {
       const V3 pp = P3(p, 0);
       normal = s * normalize(v3(0.0f - pp.x, 0.0f - pp.y, 0.0f));
       return v3s(0.0f);
     }
-    case SAIL_HYPERBOLOID: {
+    case SAIL_HYPERBOLOID: if (!HAS(c.kShapes, SAIL_HYPERBOLOID)) break; {
       const V3 hit = v3s(0.0f), p1 = P3(p, 3), p2 = P3(p, 6);
       const float v = (hit.z - p1.z) / (p2.z - p1.z);
       const V3 pr = (1.0f - v) * p1 + v * p2;
@@ -696,15 +703,16 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       normal = s * L2W(normalize(cross(dpdu, dpdv)));
       return v3s(0.0f);
     }
-    case SAIL_PARABOLOID: {
+    case SAIL_PARABOLOID: if (!HAS(c.kShapes, SAIL_PARABOLOID)) break; {
       const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
       V3 dpdu, dpdv;
       paraDpD(v3s(0.0f), zMax, zMin, dpdu, dpdv);
       normal = s * L2W(normalize(cross(dpdu, dpdv)));
       return v3s(0.0f);
     }
-    default: return v3s(0.0f);
+    default: break;
   }
+  return v3s(0.0f);
 }
 
 // ---- ssutility.glsl / fresnel.glsl / microfacet.glsl / bsdf.glsl --------------------------------------------------
@@ -856,7 +864,7 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
   float pdf = 0.0f;
   V3 fs = v3s(0.0f);
   switch (cat) {
-    case SAIL_MATTE: {  // matte.glsl:8-37
+    case SAIL_MATTE: if (!HAS(c.kMats, SAIL_MATTE)) break; {  // matte.glsl:8-37
       const float kd = TP(c, m, 1), sigma = TP(c, m, 2), A = TP(c, m, 3), B = TP(c, m, 4);
       const V3 R = kd * sc;
       wi = cosineSampleHemisphere(u);
@@ -865,7 +873,7 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
       else { fs = orenNayar_f(R, A, B, wo, wi); f = orenNayar_f(kd * sc, A, B, wo, wi); }
       break;
     }
-    case SAIL_MIRROR: {  // mirror.glsl:5-17, specular_r_sample_f bsdf.glsl:93-98
+    case SAIL_MIRROR: if (!HAS(c.kMats, SAIL_MIRROR)) break; {  // mirror.glsl:5-17, specular_r_sample_f bsdf.glsl:93-98
       const float kr = TP(c, m, 1);
       const V3 R = kr * sc;
       wi = v3(-wo.x, -wo.y, wo.z);
@@ -873,12 +881,12 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
       fs = v3s(1.0f) * R / absCosTheta(wi);
       break;
     }
-    case SAIL_METAL: {  // metal.glsl:8-22
+    case SAIL_METAL: if (!HAS(c.kMats, SAIL_METAL)) break; {  // metal.glsl:8-22
       Fr fr; fr.type = 1; fr.eta = TP3(c, m, 3); fr.k = TP3(c, m, 6); fr.etaT = 0.0f;
       fs = microR_sample(sc, fr, TP(c, m, 1), TP(c, m, 2), u, wo, wi, pdf);
       break;
     }
-    case SAIL_GLASS: {  // glass.glsl:10-36
+    case SAIL_GLASS: if (!HAS(c.kMats, SAIL_GLASS)) break; {  // glass.glsl:10-36
       const float kr = TP(c, m, 1), kt = TP(c, m, 2), eta = TP(c, m, 3), ur = TP(c, m, 4), vr = TP(c, m, 5);
       if (ur < kEps && vr < kEps) {  // specular_fr_sample_f bsdf.glsl:141-158
         const float Fd = frDielectric(wo.z, 1.0f, eta);
@@ -922,6 +930,7 @@ D bool testShadow(const Ctx& c, const Ray& r) {
 // same inputs, so evaluating the contribution first changes no bit.
 D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   // randomInt(seed,0,ln) = int(random2(seed).x * ln): the same hash as the BSDF sample's first component
+  if (c.kLights == 0) return v3s(0.0f);                      // no light plugin compiled in
   const int index = to_int(u2.x * (float)c.ln);
   if (c.ln <= 0) return v3s(0.0f);
   const int catRow = (index <= 0) ? 0 : c.ln - 1;           // readInt(lights, vec2(0, index)) : integer row coord
@@ -931,7 +940,7 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   const float* L = c.lt + row * 18;
   V3 contrib = v3s(0.0f), toLight = v3s(0.0f);
   bool lit = false;
-  if (cat == SAIL_AREA) {  // light/area.glsl
+  if (cat == SAIL_AREA && HAS(c.kLights, SAIL_AREA)) {  // light/area.glsl
     const V3 em = v3(L[2], L[3], L[4]);
     V3 normal; float pdf;
     const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
@@ -939,13 +948,13 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
     const V3 nt = normalize(toLight);
     contrib = em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
     lit = true;
-  } else if (cat == SAIL_POINT) {  // light/point.glsl:13-20
+  } else if (cat == SAIL_POINT && HAS(c.kLights, SAIL_POINT)) {  // light/point.glsl:13-20
     const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
     const V3 p = from + uniformSampleSphere(u2) * 0.1f;
     toLight = p - ins.hit;
     contrib = em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
     lit = true;
-  } else if (cat == SAIL_SPOT) {  // light/spot.glsl
+  } else if (cat == SAIL_SPOT && HAS(c.kLights, SAIL_SPOT)) {  // light/spot.glsl
     const float ctw = L[1], cfs = L[2];
     const V3 from = v3(L[3], L[4], L[5]), em = v3(L[6], L[7], L[8]);
     toLight = from - ins.hit;
@@ -1014,7 +1023,7 @@ D float q8(float v) {
 #define SAIL_TRACE_MIN_WAVES 6
 #endif
 // CULL selects the padded-box pre-cull at compile time (two kernels), so small scenes carry none of its code.
-template <bool CULL>
+template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
 __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   const int ownedTile = blockIdx.x >> 4;
   const int sub = blockIdx.x & 15;
@@ -1048,6 +1057,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
   c.shadowAnyHit = A.shadowAnyHit;
   c.cullPrims = CULL ? 1 : 0;
+  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   const size_t pix = (size_t)y * A.W + x;
   float4 acc = A.accum[pix];
@@ -1089,14 +1099,21 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   }
 }
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
-  traceTile<false>(A);
+  traceTile<false, ~0u, ~0u, ~0u, ~0u>(A);
+}
+// the README Cornell box plugin set (C1/C2/C5): Cube + Sphere + Cornellbox, Matte + Mirror, uniform colours
+#ifndef SAIL_TRACE_CORNELL_MIN_WAVES
+#define SAIL_TRACE_CORNELL_MIN_WAVES 7
+#endif
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CORNELL_MIN_WAVES) sail_trace_kernel_cornell(SailTraceArgs A) {
+  traceTile<false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS>(A);
 }
 // the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
 #endif
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CULL_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
-  traceTile<true>(A);
+  traceTile<true, ~0u, ~0u, ~0u, ~0u>(A);
 }
 
 // ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
@@ -1225,10 +1242,12 @@ extern "C" __global__ void __launch_bounds__(64) sail_pick_kernel(const SailPrim
   if (i >= count) return;
   const float* q = rays + 6 * (size_t)i;
   const Ray r = mkRay(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]));
+  Ctx c;
+  c.kShapes = ~0u;
   float best = kMaxDistance;
   int bi = -1;
   for (int k = 0; k < n; k++) {
-    const float t = primT(prims[k], r, nullptr);
+    const float t = primT(c, prims[k], r, nullptr);
     if (t < best) { best = t; bi = k; }
   }
   index[i] = bi;
@@ -1261,7 +1280,8 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
 
 // ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
-  if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
+  if (A.kernelSet == SAIL_KSET_CORNELL) hipLaunchKernelGGL(sail_trace_kernel_cornell, dim3(blocks), dim3(256), 0, s, A);
+  else if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
   else hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
   return hipGetLastError();
 }

@@ -299,3 +299,12 @@ def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, 
     got, want, st, segs, _, _ = _render_both(fixtures, name, W, H, spp, B, launch=2)
     assert bit_equal(got, want).all()
     assert st.segments == segs
+
+
+# ---- plugin-set kernels: the Cornell-box kernel (C1 scenes by default) and the generic one agree bit for bit --
+@pytest.mark.parametrize("force", ["0", "1"])
+def test_plugin_set_kernels(gpu, fixtures, monkeypatch, force):
+    monkeypatch.setenv("SAIL_FORCE_GENERIC", force)
+    got, want, st, segs, _, _ = _render_both(fixtures, "C1", 56, 40, 4, 6, launch=3)
+    assert bit_equal(got, want).all()
+    assert st.segments == segs
