@@ -147,6 +147,18 @@ D float xdiv(float a, float b, double rb) {
   if (__builtin_expect(fabsf(q) < 0x1p-126f && q != 0.0f, 0)) return a / b;
   return q;
 }
+// ---- optional phase timing (tools: -DSAIL_PHASE_TIMING=1 variant builds only): per-wave s_memtime deltas
+#ifndef SAIL_PHASE_TIMING
+#define SAIL_PHASE_TIMING 0
+#endif
+#if SAIL_PHASE_TIMING
+__device__ unsigned long long g_sailPhase[8];
+struct PhaseClock { unsigned long long t, acc[8]; };
+#define PHASE_MARK(pc, k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); (pc).acc[k] += now_ - (pc).t; (pc).t = now_; } while (0)
+#else
+struct PhaseClock {};
+#define PHASE_MARK(pc, k) do { (void)(pc); } while (0)
+#endif
 struct Hit {
   float d; V3 hit, normal, dpdu, dpdv; bool into; int matRow; V3 sc, emission; int matCategory;
 };
@@ -596,9 +608,10 @@ D float closestT(const Ctx& c, const Ray& r) {
   return best;
 }
 
-// generated intersectObjects (shader.shape.js:28-51): one sweep keeps the winner's distance and local hit
-// point, then one full record is built for the winner alone
-D Hit intersectObjects(const Ctx& c, const Ray& r) {
+// generated intersectObjects (shader.shape.js:28-51), split in two: one sweep keeps the winner's distance and
+// local hit point, then one full record is built for the winner alone
+struct Sweep { float best; int bi; V3 bhl; };
+D Sweep sweepRay(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   int bi = -1;
   V3 bhl = v3s(0.0f);
@@ -616,6 +629,13 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   }
   if (bi >= 0) primT(c, c.prims[bi], r, &bhl);  // the same arithmetic again, for the winner only
 #endif
+  Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
+  return sw;
+}
+D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
+  const float best = sw.best;
+  const int bi = sw.bi;
+  const V3 bhl = sw.bhl;
   Hit h;
   h.d = best;
   h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
@@ -642,6 +662,11 @@ D Hit intersectObjects(const Ctx& c, const Ray& r) {
   h.into = dot(h.normal, r.d) < -kEps;
   if (!h.into) h.normal = -h.normal;
   return h;
+}
+D Hit intersectObjects(const Ctx& c, const Ray& r, PhaseClock& pc) {
+  const Sweep sw = sweepRay(c, r);
+  PHASE_MARK(pc, 0);  // primitive sweep
+  return hitRecord(c, r, sw);
 }
 
 // ---- sampleGeometry for area lights (shader.shape.js:53-67) -----------------------------------------------------
@@ -977,14 +1002,24 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
 }
 
 // ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
-D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigned& segs) {
+D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc);
+D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigned& segs, PhaseClock& pc) {
   V3 fpdf = v3s(1.0f), e = v3s(0.0f);
   for (int depth = 1; depth <= maxDepth; depth++) {
     segs++;
-    const Hit ins = intersectObjects(c, ray);
+    const Hit ins = intersectObjects(c, ray, pc);
+    PHASE_MARK(pc, 1);  // hit record of the winner
     const float seed = tss + (float)depth;
     if (ins.d >= kMaxDistance) break;
     if (depth == 1) { n = ins.normal; p = ins.hit; }
+    shadeBounce(c, ins, ray, seed, fpdf, e, pc);
+  }
+  return e;
+}
+
+// shade() (path.glsl:1-14) + the bounce bookkeeping of trace() (path.glsl:27-36): radiance, throughput, next ray
+D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc) {
+  {
     // shade()
     // box faces have axis-aligned unit dpdu: dot == 1 exactly, sqrt(1) == 1 and v / 1 == v bit for bit
 #if SAIL_SS_UNIT
@@ -995,20 +1030,24 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigne
 #endif
     const V3 wo = worldToLocal(-ray.d, ins.normal, ss, ts);
     // the hash is evaluated only for materials that consume it (matte/metal/glass; mirror is deterministic)
+    PHASE_MARK(pc, 2);  // shading frame
     const V2 u2 = (ins.matCategory != SAIL_MIRROR) ? random2(c, seed) : v2(0.0f, 0.0f);
+    PHASE_MARK(pc, 3);  // hash RNG
     V3 wiL, f;
     const V3 mat = material(c, ins, u2, wo, wiL, f);
     const V3 _fpdf = vclamp01(mat);
     const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
+    PHASE_MARK(pc, 4);  // BSDF sample
     V3 direct = v3s(0.0f);
     if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) direct = direct + lightSample(c, ins, u2) * f;
+    PHASE_MARK(pc, 5);  // light sample + shadow ray
     const V3 sh = ins.emission + direct;
     e = e + sh * fpdf;
     fpdf = fpdf * _fpdf;
     const float outdot = dot(ins.normal, wi);
     ray = mkRay(ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f), wi);
+    PHASE_MARK(pc, 6);  // next ray
   }
-  return e;
 }
 
 D float q8(float v) {
@@ -1066,13 +1105,18 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
   V3 nAov = v3s(0.0f), pAov = v3s(0.0f);
   unsigned segs = 0;
+  PhaseClock pc;
+#if SAIL_PHASE_TIMING
+  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
+  pc.t = __builtin_amdgcn_s_memtime();
+#endif
   for (int k = 0; k < A.spp; k++) {
     const SailSample& S = A.samples[k];
     const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
     const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     nAov = v3s(0.0f); pAov = v3s(0.0f);
-    const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs);
+    const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs, pc);
     if (A.accumMode == 0) {
       acc.x += e.x; acc.y += e.y; acc.z += e.z; acc.w += 1.0f;
     } else {
@@ -1091,6 +1135,11 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
     const V3 q = normalize(pAov);
     A.aovP[pix] = make_float4(q.x, q.y, q.z, 1.0f);
   }
+#if SAIL_PHASE_TIMING
+  PHASE_MARK(pc, 7);  // accumulate + store
+  if (lane == 0)
+    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
+#endif
   if (A.segCounter) {
     // one atomic per wave: sum the lanes' segment counts with a cross-lane reduction
     unsigned long long v = segs;
@@ -1098,6 +1147,177 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
     if (lane == 0) atomicAdd(A.segCounter, v);
   }
 }
+// Path compaction: after every primitive sweep the workgroup's 256 live paths are sorted through LDS by
+// (shape type, material) so that the hit record and the shading, the divergent half of a bounce, run on
+// waves of like paths; dead paths drop out, so whole waves idle past the end of the live range. A path's
+// state (ray, throughput, radiance, pixel, sweep result: 18 words) migrates between lanes; every path's
+// arithmetic is unchanged, so the result is bit-identical to the unsorted kernel. The radiance of a sample
+// goes back to the pixel's own lane through LDS before it is accumulated, in sample order.
+#ifndef SAIL_COMPACT
+#define SAIL_COMPACT 1
+#endif
+template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
+__device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
+  constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
+  constexpr int kFields = 18;
+  __shared__ float sSt[kFields][256];
+  __shared__ float sE[3][256];
+  __shared__ int sCnt[kKeys];
+  __shared__ int sStart[kKeys + 1];
+  const int ownedTile = blockIdx.x >> 4;
+  if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
+  const int sub = blockIdx.x & 15;
+  const int tile = A.rank + ownedTile * A.world;
+  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
+  const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
+  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * 16;
+  const int x = x0 + (li & 15), y = y0 + (li >> 4);
+  const bool valid = x < A.W && y < A.H;   // ragged tiles: invalid lanes still serve migrated paths
+
+  Ctx c;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow;
+  c.prims = A.prims;
+  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
+  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
+  c.fcx = 0.0f; c.fcy = 0.0f;
+  c.shadowAnyHit = A.shadowAnyHit;
+  c.cullPrims = CULL ? 1 : 0;
+  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
+
+  if (li < kKeys) sCnt[li] = 0;
+  __syncthreads();
+  const size_t pixG = (size_t)y * A.W + x;
+  float4 acc = valid ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
+  const bool tri0 = s + t <= 1.0f;
+  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
+  unsigned segs = 0;
+  PhaseClock pc;
+#if SAIL_PHASE_TIMING
+  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
+  pc.t = __builtin_amdgcn_s_memtime();
+#endif
+  for (int k = 0; k < A.spp; k++) {
+    const SailSample& S = A.samples[k];
+    const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
+    bool alive = valid;
+    int pixel = li;
+    Ray ray;
+    {
+      const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
+      const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
+      ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
+    }
+    V3 fpdf = v3s(1.0f), e = v3s(0.0f);
+    for (int depth = 1; depth <= A.maxBounces; depth++) {
+      Sweep sw;
+      sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
+      int key = 0;
+      if (alive) {
+        segs++;
+        sw = sweepRay(c, ray);
+        if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
+          sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
+          if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
+            const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
+            const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
+            if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+            if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+          }
+          alive = false;
+        } else {
+          const SailPrim& p = c.prims[sw.bi];
+          int mc = to_int(TP(c, p.matRow, 0));
+          mc = (mc >= 0 && mc < 5) ? mc : 0;
+          key = 1 + p.type * 5 + mc;
+        }
+      }
+      PHASE_MARK(pc, 0);
+      // ---- counting sort of the live paths by key (LDS atomics for the per-key rank, one wave scans)
+      int rank = 0;
+      if (alive) rank = atomicAdd(&sCnt[key], 1);
+      __syncthreads();
+      if (wave == 0) {
+        const int v = sCnt[lane];
+        int incl = v;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += u;
+        }
+        sStart[lane] = incl - v;
+        if (lane == 63) sStart[kKeys] = incl;
+        sCnt[lane] = 0;
+      }
+      __syncthreads();
+      const int nAlive = sStart[kKeys];
+      if (alive) {
+        const int d = sStart[key] + rank;
+        sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
+        sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
+        sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
+        sSt[9][d] = e.x; sSt[10][d] = e.y; sSt[11][d] = e.z;
+        sSt[12][d] = __int_as_float(pixel); sSt[13][d] = __int_as_float(sw.bi); sSt[14][d] = sw.best;
+        sSt[15][d] = sw.bhl.x; sSt[16][d] = sw.bhl.y; sSt[17][d] = sw.bhl.z;
+      }
+      __syncthreads();
+      alive = li < nAlive;
+      PHASE_MARK(pc, 7);
+      if (alive) {
+        ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
+        ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
+        ray.rx = ray.ry = ray.rz = 0.0;  // not used past the sweep: the next ray is rebuilt by mkRay
+        fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
+        e = v3(sSt[9][li], sSt[10][li], sSt[11][li]);
+        pixel = __float_as_int(sSt[12][li]);
+        sw.bi = __float_as_int(sSt[13][li]); sw.best = sSt[14][li];
+        sw.bhl = v3(sSt[15][li], sSt[16][li], sSt[17][li]);
+        c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
+        c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
+        const Hit ins = hitRecord(c, ray, sw);
+        PHASE_MARK(pc, 1);
+        if (depth == 1 && aovSample) {
+          const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
+          const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
+          if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+          if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+        }
+        shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+      }
+    }
+    if (alive) { sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z; }
+    __syncthreads();
+    if (valid) {
+      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
+      if (A.accumMode == 0) {
+        acc.x += er.x; acc.y += er.y; acc.z += er.z; acc.w += 1.0f;
+      } else {
+        const float w = S.mixw;
+        float mx = er.x * (1.0f - w) + acc.x * w, my = er.y * (1.0f - w) + acc.y * w, mz = er.z * (1.0f - w) + acc.z * w;
+        if (A.accumMode == 2) { mx = q8(mx); my = q8(my); mz = q8(mz); }
+        acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
+      }
+    }
+    __syncthreads();
+  }
+  if (valid) A.accum[pixG] = acc;
+#if SAIL_PHASE_TIMING
+  if (lane == 0)
+    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
+#endif
+  if (A.segCounter) {
+    unsigned long long v = segs;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) atomicAdd(A.segCounter, v);
+  }
+}
+// Compaction pays where shading diverges and the sweep is short (the Cornell kernel: C2 +6 %); in the generic
+// and pre-cull kernels its extra live state costs more in spills than it saves (C3 -4 %, C4 -14 %, measured).
+#if SAIL_COMPACT
+#define SAIL_TILE_SMALL traceTileCompact
+#else
+#define SAIL_TILE_SMALL traceTile
+#endif
+
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
   traceTile<false, ~0u, ~0u, ~0u, ~0u>(A);
 }
@@ -1106,7 +1326,7 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_tra
 #define SAIL_TRACE_CORNELL_MIN_WAVES 7
 #endif
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CORNELL_MIN_WAVES) sail_trace_kernel_cornell(SailTraceArgs A) {
-  traceTile<false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS>(A);
+  SAIL_TILE_SMALL<false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS>(A);
 }
 // the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
@@ -1277,6 +1497,18 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
   }
   out[i] = r;
 }
+
+#if SAIL_PHASE_TIMING
+// phase-timing readout for the variant harness (tools/variant_bench.py --phases)
+extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sailPhase), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
