@@ -1159,7 +1159,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
-  constexpr int kFields = 18;
+  constexpr int kFields = 15;
   __shared__ float sSt[kFields][256];
   __shared__ float sE[3][256];
   __shared__ int sCnt[kKeys];
@@ -1208,7 +1208,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
       ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     }
-    V3 fpdf = v3s(1.0f), e = v3s(0.0f);
+    V3 fpdf = v3s(1.0f);
+    // the path's radiance lives in LDS at its pixel: one path per pixel, updated in bounce order
+    sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f;
     for (int depth = 1; depth <= A.maxBounces; depth++) {
       Sweep sw;
       sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
@@ -1217,7 +1219,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         segs++;
         sw = sweepRay(c, ray);
         if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
-          sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
           if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
             const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
             const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
@@ -1255,9 +1256,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
         sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
         sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
-        sSt[9][d] = e.x; sSt[10][d] = e.y; sSt[11][d] = e.z;
-        sSt[12][d] = __int_as_float(pixel); sSt[13][d] = __int_as_float(sw.bi); sSt[14][d] = sw.best;
-        sSt[15][d] = sw.bhl.x; sSt[16][d] = sw.bhl.y; sSt[17][d] = sw.bhl.z;
+        sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
+        sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
       }
       __syncthreads();
       alive = li < nAlive;
@@ -1267,10 +1267,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
         ray.rx = ray.ry = ray.rz = 0.0;  // not used past the sweep: the next ray is rebuilt by mkRay
         fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
-        e = v3(sSt[9][li], sSt[10][li], sSt[11][li]);
-        pixel = __float_as_int(sSt[12][li]);
-        sw.bi = __float_as_int(sSt[13][li]); sw.best = sSt[14][li];
-        sw.bhl = v3(sSt[15][li], sSt[16][li], sSt[17][li]);
+        pixel = __float_as_int(sSt[9][li]);
+        sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
+        sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
         const Hit ins = hitRecord(c, ray, sw);
@@ -1281,10 +1280,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
+        V3 e = v3(sE[0][pixel], sE[1][pixel], sE[2][pixel]);
         shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+        sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
       }
     }
-    if (alive) { sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z; }
     __syncthreads();
     if (valid) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
