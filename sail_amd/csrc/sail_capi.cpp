@@ -149,6 +149,7 @@ int kernelSetFor(const sail_ctx* c) {
   if ((p.shape_mask & ~SAIL_KSET_CORNELL_SHAPES) == 0 && (p.material_mask & ~SAIL_KSET_CORNELL_MATS) == 0 &&
       (p.texture_mask & ~SAIL_KSET_CORNELL_TEX) == 0 && lightsOk && SAIL_KSET_CORNELL_LIGHTS == 0 && c->ln == 0)
     return SAIL_KSET_CORNELL;
+  if ((p.shape_mask & ~SAIL_KSET_ROOM_SHAPES) == 0) return SAIL_KSET_ROOM;
   return SAIL_KSET_GENERIC;
 }
 

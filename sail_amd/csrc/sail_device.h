@@ -65,11 +65,16 @@ struct SailTraceArgs {
 
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a
 // set's masks may use that set's kernel; everything else runs the generic one.
-enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1 };
+enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
 #define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))
 #define SAIL_KSET_CORNELL_MATS ((1u << SAIL_MATTE) | (1u << SAIL_MIRROR))
 #define SAIL_KSET_CORNELL_TEX 0u
 #define SAIL_KSET_CORNELL_LIGHTS 0u
+// rooms of boxes, spheres and rectangle lights (C3 materials demo, the UI demo): no quadrics or disks
+#define SAIL_KSET_ROOM_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_RECTANGLE) | (1u << SAIL_CORNELLBOX))
+#define SAIL_KSET_ROOM_MATS 0xffffffffu
+#define SAIL_KSET_ROOM_TEX 0xffffffffu
+#define SAIL_KSET_ROOM_LIGHTS 0xffffffffu
 
 struct SailFilterArgs {
   const float4* accum;

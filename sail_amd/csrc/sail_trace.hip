@@ -1332,6 +1332,15 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CORNELL_MIN_WAVES) 
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
 #endif
+#ifndef SAIL_TRACE_ROOM_MIN_WAVES
+#define SAIL_TRACE_ROOM_MIN_WAVES 6
+#endif
+#ifndef SAIL_ROOM_TILE
+#define SAIL_ROOM_TILE traceTile
+#endif
+extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_ROOM_MIN_WAVES) sail_trace_kernel_room(SailTraceArgs A) {
+  SAIL_ROOM_TILE<false, SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS>(A);
+}
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CULL_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
   traceTile<true, ~0u, ~0u, ~0u, ~0u>(A);
 }
@@ -1513,6 +1522,7 @@ extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
 // ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
   if (A.kernelSet == SAIL_KSET_CORNELL) hipLaunchKernelGGL(sail_trace_kernel_cornell, dim3(blocks), dim3(256), 0, s, A);
+  else if (A.kernelSet == SAIL_KSET_ROOM) hipLaunchKernelGGL(sail_trace_kernel_room, dim3(blocks), dim3(256), 0, s, A);
   else if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
   else hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
   return hipGetLastError();
