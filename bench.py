@@ -45,6 +45,39 @@ def load_scene(name="C1"):
         return json.load(f)[name]
 
 
+def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0):
+    """BASELINE.json's CPU baseline: the single-threaded JS/Node software shader (oracle/sail_soft.js, bit-exact
+    with the C++ oracle and the HIP kernel) timed on the host on a bounded sample of the same frame: 32x32
+    crops spiralling out from the centre, 8 spp each, until ~budget_s of render time (node start excluded)."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node") or shutil.which("nodejs")
+    if node is None:
+        return None
+    spp, c = 8, 32
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    cx, cy = (W - c) // 2, (H - c) // 2
+    offsets = sorted(((dx, dy) for dx in range(-9, 10) for dy in range(-9, 10)), key=lambda d: d[0] ** 2 + d[1] ** 2)
+    crops = [[cx + dx * c, cy + dy * c, c, c] for dx, dy in offsets
+             if 0 <= cx + dx * c and 0 <= cy + dy * c and cx + dx * c + c <= W and cy + dy * c + c <= H]
+    job = {"objects": sc["objects"], "n": sc["n"], "texparams": sc["texparams"], "tn": sc["tn"], "lights": sc["lights"],
+           "ln": sc["ln"], "masks": list(masks), "W": W, "H": H, "inv": [float(v) for v in inv.reshape(-1)],
+           "seeds": [float(v) for v in seeds], "eye": sc["eye"], "spp": spp, "maxBounces": B, "accumMode": 0,
+           "crops": crops, "budgetSeconds": budget_s}
+    with tempfile.TemporaryDirectory() as td:
+        jp = os.path.join(td, "job.json")
+        with open(jp, "w") as f:
+            json.dump(job, f)
+        out = subprocess.run([node, os.path.join(ROOT, "oracle", "sail_soft.js"), jp, os.path.join(td, "o")],
+                             capture_output=True, text=True, timeout=budget_s * 10 + 60, check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    return {"value": r["segments"] / r["seconds"] / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "implementation": f"oracle/sail_soft.js on Node {r['node']}, single thread",
+            "sample": f"{r['crops']} centre-out {c}x{c} crops of the frame, {spp} spp x {B} bounces = {r['segments']} "
+                      f"segments (exact count) in {r['seconds']:.2f} s"}
+
+
 def cpu_baseline(sc, masks, mvp, W, H, B, budget_s=10.0):
     """The CPU oracle (single-threaded C++ restatement of the shader) timed on a bounded sample of the same
     frame: 32x32 crops spiralling out from the centre, 4 spp each, until ~budget_s of CPU work."""
@@ -54,7 +87,7 @@ def cpu_baseline(sc, masks, mvp, W, H, B, budget_s=10.0):
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     acc = np.zeros((H, W, 4), np.float32)
     cx, cy = (W - c) // 2, (H - c) // 2
-    offsets = sorted(((dx, dy) for dx in range(-6, 7) for dy in range(-6, 7)), key=lambda d: d[0] ** 2 + d[1] ** 2)
+    offsets = sorted(((dx, dy) for dx in range(-9, 10) for dy in range(-9, 10)), key=lambda d: d[0] ** 2 + d[1] ** 2)
     oracle.reset_counters()
     t0 = time.perf_counter()
     crops = 0
@@ -219,7 +252,10 @@ def main():
             },
         }
         if not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(sc, masks, mvp, W, H, B)
+            # the north star's JS/Node software shader; the C++ restatement is timed beside it for reference
+            cpp = cpu_baseline(sc, masks, mvp, W, H, B, budget_s=5.0)
+            js = cpu_baseline_js(sc, masks, mvp, W, H, B)
+            rec["cpu_baseline"] = dict(js, cpp_port=cpp) if js else cpp
         print(json.dumps(rec), flush=True)
     ctx.close()
     if dist is not None:
