@@ -245,7 +245,7 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "ops_per_segment": round(ops_seg, 2), "kernel": "sail_trace_kernel",
+                "ops_per_segment": round(ops_seg, 2), "kernel": ctx.kernel_name(),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},

@@ -139,6 +139,9 @@ int sail_partition_tiles(int width, int height, int rank, int world, int* out_xy
  * 6 atan 7 sqrt 8 x/y); for the CPU/GPU bit-parity test */
 int sail_math_probe(int fn, const float* x, const float* y, float* out, int count);
 int sail_abi_version(void);
+/* the trace kernel the context's current scene launches (a plugin-set specialisation, like the reference's
+ * per-scene generated program): writes its name (e.g. "sail_trace_kernel_cornell") into name[len] */
+int sail_kernel_name(sail_ctx* ctx, char* name, int len);
 
 #ifdef __cplusplus
 }

@@ -445,6 +445,17 @@ extern "C" {
 
 int sail_abi_version(void) { return SAIL_ABI_VERSION; }
 
+int sail_kernel_name(sail_ctx* c, char* name, int len) {
+  if (!c || !name || len <= 0) return SAIL_E_INVALID;
+  if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_kernel_name: no scene");
+  const int set = kernelSetFor(c);
+  const char* k = set == SAIL_KSET_CORNELL ? "sail_trace_kernel_cornell"
+                  : set == SAIL_KSET_ROOM ? "sail_trace_kernel_room"
+                  : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
+  snprintf(name, (size_t)len, "%s", k);
+  return SAIL_OK;
+}
+
 int sail_device_count(int* count) {
   if (!count) return SAIL_E_INVALID;
   int n = 0;

@@ -292,7 +292,7 @@ def test_pick_matches_oracle(gpu, fixtures, name):
 
 # ---- the padded-box pre-cull (scenes with >= 8 primitives) must not change a single bit -----------------------
 @pytest.mark.parametrize("name,W,H,spp,B", [("C1", 48, 32, 4, 5), ("C3", 40, 40, 3, 8), ("ALL", 40, 32, 3, 6),
-                                            ("UI", 32, 32, 3, 5)])
+                                            ("UI", 32, 32, 3, 5), ("C4", 24, 24, 2, 12)])
 @pytest.mark.parametrize("cull", ["0", "1000"])
 def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, B, cull):
     monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)   # 0: cull every scene, 1000: never
@@ -308,3 +308,14 @@ def test_plugin_set_kernels(gpu, fixtures, monkeypatch, force):
     got, want, st, segs, _, _ = _render_both(fixtures, "C1", 56, 40, 4, 6, launch=3)
     assert bit_equal(got, want).all()
     assert st.segments == segs
+
+
+def test_kernel_selection(gpu, fixtures):
+    """plugin-set dispatch: the smallest precompiled kernel covering the scene (sail_kernel_name)"""
+    want = {"C1": "sail_trace_kernel_cornell", "C1g": "sail_trace_kernel_cornell", "C3": "sail_trace_kernel_room",
+            "UI": "sail_trace_kernel_room", "C4": "sail_trace_kernel_cull"}
+    for name, k in want.items():
+        ctx = capi.Context(8, 8)
+        ctx.set_scene_dict(fixtures["scenes"][name])
+        assert ctx.kernel_name() == k, name
+        ctx.close()
