@@ -31,7 +31,10 @@ CONFIGS = {
     "C2": {"workload": "cornell_box_readme_C2", "desc": "README Cornell box", "scene": "C1", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
     "C3": {"workload": "materials_demo_C3", "desc": "materials demo", "scene": "C3", "width": 1920, "height": 1080, "bounces": 8, "spp": 1024},
     "C4": {"workload": "random64_C4", "desc": "random-64 primitives", "scene": "C4", "width": 3840, "height": 2160, "bounces": 12, "spp": 256},
-    "C5": {"workload": "cornell_box_converged_C5", "desc": "README Cornell box (converged)", "scene": "C1", "width": 1920, "height": 1080, "bounces": 16, "spp": 65536},
+    # converged render: sample split across ranks (full occupancy per GPU, RCCL sample-sum reduce), then the
+    # Gaussian reconstruction filter on rank 0 inside the step (BASELINE configs[4])
+    "C5": {"workload": "cornell_box_converged_C5", "desc": "README Cornell box (converged)", "scene": "C1g", "width": 1920,
+           "height": 1080, "bounces": 16, "spp": 65536, "partition": "samples", "filter": "gaussian"},
 }
 CONFIG = CONFIGS["C2"]
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
@@ -170,8 +173,11 @@ def main():
     ctx = capi.Context(W, H, device=local_rank)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
+    part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
+    flt = sc.get("filter") if cfg.get("filter") else None
+    fweights = np.array(flt["weights64"], dtype=np.float32) if flt else None
     if use_comm:
-        ctx.set_partition(rank, world, capi.PART_TILES)
+        ctx.set_partition(rank, world, part)
         uid = [capi.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], world, rank)
@@ -181,6 +187,8 @@ def main():
         ctx.render_schedule(inv, seeds, sc["eye"], B)
         if use_comm:
             ctx.reduce(0)
+        if flt and rank == 0:  # reconstruction filter of the reduced frame (window.glsl, gaussian r = 2)
+            ctx.filter(capi.FILTER_WINDOW, fweights, flt["radius"][0], flt["radius"][1], 2.2)
 
     def barrier_sync():
         ctx.sync()
@@ -214,7 +222,7 @@ def main():
     if rank == 0:
         avg_launch_s = (kernel_ms / max(launches, 1)) / 1e3
         # this rank's pixels per launch (rank 0 at N = 1: the full frame)
-        tiles_px = W * H if world == 1 else None
+        tiles_px = W * H if (world == 1 or part == capi.PART_SAMPLES) else None
         if tiles_px is None:
             tx, ty = (W + 63) // 64, (H + 63) // 64
             tiles_px = 0
@@ -251,6 +259,13 @@ def main():
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},
             },
         }
+        if flt:
+            fms = ctx.filter_ms()
+            fbytes = W * H * (16 + 16)  # mean-image read once from HBM (taps hit L2) + float4 write
+            rec["filter"] = {"kind": flt["name"], "kernel": "sail_filter_kernel", "avg_ms": round(fms, 4),
+                             "bound": "hbm", "bytes_per_pass": fbytes, "achieved": round(fbytes / (fms * 1e-3) / 1e9, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fbytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            rec["config"]["partition"] = f"{cfg.get('partition', 'tiles')}x{world}"
         if not args.no_cpu_baseline and world == 1:
             # the north star's JS/Node software shader; the C++ restatement is timed beside it for reference
             cpp = cpu_baseline(sc, masks, mvp, W, H, B, budget_s=5.0)

@@ -142,6 +142,8 @@ int sail_abi_version(void);
 /* the trace kernel the context's current scene launches (a plugin-set specialisation, like the reference's
  * per-scene generated program): writes its name (e.g. "sail_trace_kernel_cornell") into name[len] */
 int sail_kernel_name(sail_ctx* ctx, char* name, int len);
+/* device time of the last sail_filter pass (HIP events around the kernel), for the stencil's roofline */
+int sail_filter_ms(sail_ctx* ctx, double* ms);
 
 #ifdef __cplusplus
 }

@@ -30,7 +30,7 @@ EXPORTS = (
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
-    "sail_math_probe", "sail_pick", "sail_kernel_name",
+    "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
     "sail_abi_version",
 )
 
@@ -114,6 +114,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_abi_version": (ctypes.c_int, []),
         "sail_pick": (ctypes.c_int, [vp, f32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), f32p]),
         "sail_kernel_name": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int]),
+        "sail_filter_ms": (ctypes.c_int, [vp, f64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -297,6 +298,11 @@ class Context:
         t = np.zeros(len(r), dtype=np.float32)
         self._check(self.lib.sail_pick(self.h, _ptr(r), len(r), _ptr(idx, ctypes.c_int32), _ptr(t)), "sail_pick")
         return idx, t
+
+    def filter_ms(self) -> float:
+        v = ctypes.c_double()
+        self._check(self.lib.sail_filter_ms(self.h, ctypes.byref(v)), "sail_filter_ms")
+        return v.value
 
     def kernel_name(self) -> str:
         buf = ctypes.create_string_buffer(64)

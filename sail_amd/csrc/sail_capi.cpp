@@ -117,6 +117,7 @@ struct sail_ctx {
   std::vector<hipEvent_t> evPool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   double kernelMs = 0.0, lastLaunchMs = 0.0;
+  double lastFilterMs = 0.0;  // device time of the last display-filter pass
   uint32_t launches = 0;
   nccl_comm_t comm = nullptr;
   int commRanks = 0, commRank = 0;
@@ -445,6 +446,12 @@ extern "C" {
 
 int sail_abi_version(void) { return SAIL_ABI_VERSION; }
 
+int sail_filter_ms(sail_ctx* c, double* ms) {
+  if (!c || !ms) return SAIL_E_INVALID;
+  *ms = c->lastFilterMs;
+  return SAIL_OK;
+}
+
 int sail_kernel_name(sail_ctx* c, char* name, int len) {
   if (!c || !name || len <= 0) return SAIL_E_INVALID;
   if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_kernel_name: no scene");
@@ -701,8 +708,27 @@ int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float r
   A.count = cnt; A.invCount = 1.0f / cnt;
   if (weights16) memcpy(A.weights, weights16, sizeof A.weights);
   A.rx = rx; A.ry = ry; A.gammaC = gammaC;
-  hipError_t e = sail_launch_filter(A, c->stream);
+  // window taps reach 0.875 r pixels (offsets (j + 0.5) r / 4, j < 4) + the bilinear footprint + rounding
+  if (kind == SAIL_FILTER_WINDOW) {
+    const float r = fmaxf(fabsf(rx), fabsf(ry));
+    const int h = (r == r) ? (int)ceilf(0.875f * r) + 2 : 99;
+    A.halo = h <= 8 ? h : 0;
+  }
+  hipEvent_t f0 = nullptr, f1 = nullptr;
+  int rcE = getEvent(c, &f0);
+  if (rcE == SAIL_OK) rcE = getEvent(c, &f1);
+  if (rcE != SAIL_OK) return rcE;
+  hipError_t e = hipEventRecord(f0, c->stream);
+  if (e == hipSuccess) e = sail_launch_filter(A, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(f1, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) {
+    float ms = 0.0f;
+    e = hipEventElapsedTime(&ms, f0, f1);
+    c->lastFilterMs = ms;
+  }
+  c->evPool.push_back(f0);
+  c->evPool.push_back(f1);
   if (e == hipSuccess && out) e = hipMemcpy(out, dOut, np * sizeof(float4), hipMemcpyDeviceToHost);
   if (e == hipSuccess && out8) e = hipMemcpy(out8, dOut8, np * 4, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(c, SAIL_E_HIP, "sail_filter: %s", hipGetErrorString(e));

@@ -89,4 +89,5 @@ struct SailFilterArgs {
   float count;
   float weights[16];
   float rx, ry, gammaC;
+  int halo;                 // window filters: LDS tile halo in pixels (0: taps read global memory)
 };

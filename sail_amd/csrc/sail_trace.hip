@@ -1375,10 +1375,37 @@ D V3 sample(const SailFilterArgs& A, const float4* img, bool mean, float u, floa
                 texel(A, img, mean, t.xb, t.yb), t.a, t.b);
 }
 D float dot4(V3 t, float w) { return t.x * t.x + t.y * t.y + t.z * t.z + w * w; }
+// window filters: the workgroup's 16x16 pixels plus a halo of mean texels staged in LDS once (one divide per
+// texel instead of one per tap read); taps that would leave the tile read global memory as before
+constexpr int kFiltMaxT = 32;
+struct FiltTile { const float* r; const float* g; const float* b; int x0, y0, T; };
+D V3 sampleTile(const SailFilterArgs& A, const FiltTile& tl, float u, float v) {
+  const float fx = u * (float)A.W - 0.5f, fy = v * (float)A.H - 0.5f;
+  const float x0f = floorf(fx), y0f = floorf(fy);
+  const float a = fx - x0f, b = fy - y0f;
+  const int lx = (int)x0f - tl.x0, ly = (int)y0f - tl.y0;
+  if (lx < 0 || ly < 0 || lx + 1 >= tl.T || ly + 1 >= tl.T) return sample(A, A.accum, true, u, v);
+  const int i00 = ly * tl.T + lx, i01 = i00 + tl.T;
+  return bilerp(v3(tl.r[i00], tl.g[i00], tl.b[i00]), v3(tl.r[i00 + 1], tl.g[i00 + 1], tl.b[i00 + 1]),
+                v3(tl.r[i01], tl.g[i01], tl.b[i01]), v3(tl.r[i01 + 1], tl.g[i01 + 1], tl.b[i01 + 1]), a, b);
+}
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterArgs A) {
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  __shared__ float sTR[kFiltMaxT * kFiltMaxT], sTG[kFiltMaxT * kFiltMaxT], sTB[kFiltMaxT * kFiltMaxT];
+  FiltTile tl;
+  tl.r = sTR; tl.g = sTG; tl.b = sTB;
+  tl.T = 16 + 2 * A.halo;
+  tl.x0 = (int)blockIdx.x * 16 - A.halo; tl.y0 = (int)blockIdx.y * 16 - A.halo;
+  if (A.kind == 3 && A.halo > 0) {  // uniform over the grid
+    for (int i = threadIdx.x; i < tl.T * tl.T; i += 256) {
+      const int ly = i / tl.T, lx = i - ly * tl.T;
+      const V3 m = texel(A, A.accum, true, wrapi(tl.x0 + lx, A.W), wrapi(tl.y0 + ly, A.H));  // REPEAT wrap
+      sTR[i] = m.x; sTG[i] = m.y; sTB[i] = m.z;
+    }
+    __syncthreads();
+  }
   if (x >= A.W || y >= A.H) return;
   const float tcx = ((float)x + 0.5f) / (float)A.W, tcy = ((float)y + 0.5f) / (float)A.H;
   float o[4] = {0.0f, 0.0f, 0.0f, 1.0f};
@@ -1407,7 +1434,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
           const float v = (q & 1) ? tcy - oy : tcy + oy;
           if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) continue;
           count++;
-          tmp = tmp + sample(A, A.accum, true, u, v);
+          tmp = tmp + (A.halo > 0 ? sampleTile(A, tl, u, v) : sample(A, A.accum, true, u, v));
         }
         const float weight = A.weights[i * j + j];
         weightSum += weight * (float)count;
