@@ -16,6 +16,7 @@
 // launch wrappers defined next to the kernels (sail_trace.hip)
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
+hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
 hipError_t sail_launch_pick(const SailPrim* prims, int n, const float* rays, int count, int32_t* index, float* t,
                             hipStream_t s);
@@ -108,6 +109,10 @@ struct sail_ctx {
   int shadowAnyHit = 0;
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
+  int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
+  int numCUs = 256;
+  float4* stage = nullptr;  // sample-group staging, allocated on first use
+  size_t stageBytes = 0;
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
   int launchSpp = 32;
@@ -428,10 +433,35 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.cullPrims = c->n >= c->cullMinPrims;
     A.kernelSet = kernelSetFor(c);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
+    // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
+    // = 1,016 workgroups = 4 waves per SIMD); split the launch's samples over G workgroups per block so
+    // that about 4 rounds of 7-wave-per-SIMD residency are queued, and add the staged samples in order.
+    int G = 1;
+    {
+      const long long waves = (long long)owned * 16 * 4;
+      const long long target = (long long)c->numCUs * 4 * 7 * 4;
+      G = c->forceGroups > 0 ? c->forceGroups : (int)((target + waves - 1) / waves);
+      if (G > nspp) G = nspp;
+      if (G < 1) G = 1;
+    }
+    A.groupSpp = (nspp + G - 1) / G;
+    A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
+    A.stageStride = (long long)owned * 4096;
+    if (A.sampleGroups > 1) {
+      const size_t need = (size_t)A.stageStride * (size_t)c->launchSpp * sizeof(float4);
+      if (need > c->stageBytes) {
+        if (c->stage) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->stage)); c->stage = nullptr; }
+        c->stageBytes = 0;
+        if (hipMalloc(&c->stage, need) != hipSuccess) { c->stage = nullptr; return fail(c, SAIL_E_OOM, "sample-group stage"); }
+        c->stageBytes = need;
+      }
+      A.stage = c->stage;
+    }
     hipEvent_t e0, e1;
     if ((rc = getEvent(c, &e0)) || (rc = getEvent(c, &e1))) return rc;
     HIPCHK(c, hipEventRecord(e0, c->stream));
-    HIPCHK(c, sail_launch_trace(A, owned * 16, c->stream));
+    HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
+    if (A.sampleGroups > 1) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending.emplace_back(e0, e1);
     c->launches++;
@@ -485,12 +515,17 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
   c->device = device; c->W = width; c->H = height; c->flags = flags;
   if (const char* e = getenv("SAIL_CULL_MIN_PRIMS")) c->cullMinPrims = atoi(e);  // tests force the pre-cull on/off
   if (const char* e = getenv("SAIL_FORCE_GENERIC")) c->forceGeneric = atoi(e);
+  if (const char* e = getenv("SAIL_SAMPLE_GROUPS")) c->forceGroups = atoi(e);
   auto bail = [&](int code, const char* what) {
     g_create_error = std::string("sail_create: ") + what;
     sail_destroy(c);
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(SAIL_E_HIP, "hipSetDevice");
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) c->numCUs = cus;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(SAIL_E_HIP, "stream");
   const size_t bytes = (size_t)width * height * sizeof(float4);
   if (hipMalloc(&c->accum, bytes) != hipSuccess) return bail(SAIL_E_OOM, "accumulator");
@@ -513,7 +548,7 @@ void sail_destroy(sail_ctx* c) {
   if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
   for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->evPool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->accum, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
+  void* bufs[] = {c->accum, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;

@@ -61,6 +61,12 @@ struct SailTraceArgs {
   int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
   int cullPrims;            // 1: padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test
   int kernelSet;            // SAIL_KSET_*: the precompiled plugin-set kernel to launch
+  // sample groups (small per-rank frames): sampleGroups workgroups share each 16x16 block, group g renders
+  // samples [g*groupSpp, (g+1)*groupSpp) into stage[k * stageStride + slot]; sail_accum_kernel then adds them
+  // to the accumulator in sample order, so the sums are bit-identical to one workgroup doing all samples
+  int sampleGroups, groupSpp;
+  float4* stage;
+  long long stageStride;    // slots per sample = ownedTiles * 4096
 };
 
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a

@@ -151,8 +151,10 @@ D float xdiv(float a, float b, double rb) {
 #ifndef SAIL_PHASE_TIMING
 #define SAIL_PHASE_TIMING 0
 #endif
-#if SAIL_PHASE_TIMING
+#if SAIL_PHASE_TIMING || SAIL_CULL_STATS
 __device__ unsigned long long g_sailPhase[8];
+#endif
+#if SAIL_PHASE_TIMING
 struct PhaseClock { unsigned long long t, acc[8]; };
 #define PHASE_MARK(pc, k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); (pc).acc[k] += now_ - (pc).t; (pc).t = now_; } while (0)
 #else
@@ -594,11 +596,31 @@ D bool padHit(const SailPrim& p, const Ray& r, float best) {
   return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > best * 1.0001f + 1e-4f);
 }
 
+// -DSAIL_CULL_STATS=1 (variant builds only): per (wave, primitive) counts of pre-cull outcomes in g_sailPhase:
+// [0] tests, [1] tests where some lane passed, [2] passing lanes, [3] active lanes
+#ifndef SAIL_CULL_STATS
+#define SAIL_CULL_STATS 0
+#endif
+#if SAIL_CULL_STATS
+D void cullStat(bool pass) {
+  const unsigned long long act = __ballot(1), m = __ballot(pass);
+  if (__lane_id() == (unsigned)(__ffsll((long long)act) - 1)) {
+    atomicAdd(&g_sailPhase[0], 1ull);
+    if (m) atomicAdd(&g_sailPhase[1], 1ull);
+    atomicAdd(&g_sailPhase[2], (unsigned long long)__popcll(m));
+    atomicAdd(&g_sailPhase[3], (unsigned long long)__popcll(act));
+  }
+}
+#define CULL_TEST(c, p, r, best) ([&]() { const bool ok_ = padHit(p, r, best); cullStat(ok_); return ok_; }())
+#else
+#define CULL_TEST(c, p, r, best) padHit(p, r, best)
+#endif
+
 // closest distance only (shadow rays, testShadow shader.light.js:24-31)
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
+    if (c.cullPrims && !CULL_TEST(c, c.prims[i], r, best)) continue;
     const float t = primT(c, c.prims[i], r, nullptr);
     if (t < best) {
       best = t;
@@ -617,7 +639,7 @@ D Sweep sweepRay(const Ctx& c, const Ray& r) {
   V3 bhl = v3s(0.0f);
 #if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !padHit(c.prims[i], r, best)) continue;
+    if (c.cullPrims && !CULL_TEST(c, c.prims[i], r, best)) continue;
     V3 hl = v3s(0.0f);
     const float t = primT(c, c.prims[i], r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
@@ -1054,6 +1076,30 @@ D float q8(float v) {
   v = fmin_(fmax_(v, 0.0f), 1.0f);
   return floorf(v * 255.0f + 0.5f) / 255.0f;
 }
+// fstrace.glsl:13 accumulation of one sample (SUM: running sums + count; MIX / COMPAT8: the reference's
+// mix(e, cache, k/(k+1)), COMPAT8 through the UNORM8 frame store)
+D void accumulateSample(float4& acc, V3 e, const SailSample& S, int mode) {
+  if (mode == 0) {
+    acc.x += e.x; acc.y += e.y; acc.z += e.z; acc.w += 1.0f;
+  } else {
+    const float w = S.mixw;
+    float mx = e.x * (1.0f - w) + acc.x * w, my = e.y * (1.0f - w) + acc.y * w, mz = e.z * (1.0f - w) + acc.z * w;
+    if (mode == 2) { mx = q8(mx); my = q8(my); mz = q8(mz); }
+    acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
+  }
+}
+// the workgroup's 16x16 block and sample range: blockIdx.x = group * (ownedTiles * 16) + block
+struct TileWork { int ownedTile, sub, kBeg, kEnd; long long slotBase; };
+D TileWork tileWork(const SailTraceArgs& A) {
+  const int nb = A.ownedTiles * 16;
+  const int bid = (int)blockIdx.x % nb, group = (int)blockIdx.x / nb;
+  TileWork w;
+  w.ownedTile = bid >> 4; w.sub = bid & 15;
+  w.kBeg = group * A.groupSpp;
+  w.kEnd = w.kBeg + A.groupSpp < A.spp ? w.kBeg + A.groupSpp : A.spp;
+  w.slotBase = (long long)bid * 256;
+  return w;
+}
 
 }  // namespace
 
@@ -1064,8 +1110,9 @@ D float q8(float v) {
 // CULL selects the padded-box pre-cull at compile time (two kernels), so small scenes carry none of its code.
 template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
 __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
-  const int ownedTile = blockIdx.x >> 4;
-  const int sub = blockIdx.x & 15;
+  const TileWork tw = tileWork(A);
+  const int ownedTile = tw.ownedTile;
+  const int sub = tw.sub;
   const int tile = A.rank + ownedTile * A.world;
   const int tx = tile % A.tilesX, ty = tile / A.tilesX;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1099,10 +1146,12 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   const size_t pix = (size_t)y * A.W + x;
-  float4 acc = A.accum[pix];
+  const bool grouped = A.sampleGroups > 1;
+  float4 acc = grouped ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : A.accum[pix];
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
+  const bool aovGroup = tw.kEnd == A.spp;  // the group holding the launch's last sample writes the AOVs
   V3 nAov = v3s(0.0f), pAov = v3s(0.0f);
   unsigned segs = 0;
   PhaseClock pc;
@@ -1110,28 +1159,22 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   for (int q = 0; q < 8; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
-  for (int k = 0; k < A.spp; k++) {
+  for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = A.samples[k];
     const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
     const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     nAov = v3s(0.0f); pAov = v3s(0.0f);
     const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs, pc);
-    if (A.accumMode == 0) {
-      acc.x += e.x; acc.y += e.y; acc.z += e.z; acc.w += 1.0f;
-    } else {
-      const float w = S.mixw;
-      float mx = e.x * (1.0f - w) + acc.x * w, my = e.y * (1.0f - w) + acc.y * w, mz = e.z * (1.0f - w) + acc.z * w;
-      if (A.accumMode == 2) { mx = q8(mx); my = q8(my); mz = q8(mz); }
-      acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
-    }
+    if (grouped) A.stage[(size_t)k * A.stageStride + tw.slotBase + threadIdx.x] = make_float4(e.x, e.y, e.z, 0.0f);
+    else accumulateSample(acc, e, S, A.accumMode);
   }
-  A.accum[pix] = acc;
-  if (A.aovN) {
+  if (!grouped) A.accum[pix] = acc;
+  if (A.aovN && aovGroup) {
     const V3 q = nAov / 2.0f + 0.5f;
     A.aovN[pix] = make_float4(q.x, q.y, q.z, 1.0f);
   }
-  if (A.aovP) {
+  if (A.aovP && aovGroup) {
     const V3 q = normalize(pAov);
     A.aovP[pix] = make_float4(q.x, q.y, q.z, 1.0f);
   }
@@ -1164,9 +1207,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   __shared__ float sE[3][256];
   __shared__ int sCnt[kKeys];
   __shared__ int sStart[kKeys + 1];
-  const int ownedTile = blockIdx.x >> 4;
+  const TileWork tw = tileWork(A);
+  const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
-  const int sub = blockIdx.x & 15;
+  const int sub = tw.sub;
   const int tile = A.rank + ownedTile * A.world;
   const int tx = tile % A.tilesX, ty = tile / A.tilesX;
   const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
@@ -1187,7 +1231,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (li < kKeys) sCnt[li] = 0;
   __syncthreads();
   const size_t pixG = (size_t)y * A.W + x;
-  float4 acc = valid ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const bool grouped = A.sampleGroups > 1;
+  float4 acc = (valid && !grouped) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
@@ -1197,7 +1242,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   for (int q = 0; q < 8; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
-  for (int k = 0; k < A.spp; k++) {
+  for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = A.samples[k];
     const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
     bool alive = valid;
@@ -1288,18 +1333,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     __syncthreads();
     if (valid) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
-      if (A.accumMode == 0) {
-        acc.x += er.x; acc.y += er.y; acc.z += er.z; acc.w += 1.0f;
-      } else {
-        const float w = S.mixw;
-        float mx = er.x * (1.0f - w) + acc.x * w, my = er.y * (1.0f - w) + acc.y * w, mz = er.z * (1.0f - w) + acc.z * w;
-        if (A.accumMode == 2) { mx = q8(mx); my = q8(my); mz = q8(mz); }
-        acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
-      }
+      if (grouped) A.stage[(size_t)k * A.stageStride + tw.slotBase + li] = make_float4(er.x, er.y, er.z, 0.0f);
+      else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
   }
-  if (valid) A.accum[pixG] = acc;
+  if (valid && !grouped) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
   if (lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
@@ -1343,6 +1382,25 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_ROOM_MIN_WAVES) sai
 }
 extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CULL_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
   traceTile<true, ~0u, ~0u, ~0u, ~0u>(A);
+}
+
+// ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
+extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {
+  const int bid = (int)blockIdx.x;
+  const int ownedTile = bid >> 4, sub = bid & 15;
+  const int tile = A.rank + ownedTile * A.world;
+  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
+  const int li = threadIdx.x;
+  const int x = tx * 64 + (sub & 3) * 16 + (li & 15), y = ty * 64 + (sub >> 2) * 16 + (li >> 4);
+  if (x >= A.W || y >= A.H) return;
+  const size_t pix = (size_t)y * A.W + x;
+  float4 acc = A.accum[pix];
+  const float4* st = A.stage + (long long)bid * 256 + li;
+  for (int k = 0; k < A.spp; k++) {
+    const float4 v = st[(size_t)k * A.stageStride];
+    accumulateSample(acc, v3(v.x, v.y, v.z), A.samples[k], A.accumMode);
+  }
+  A.accum[pix] = acc;
 }
 
 // ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
@@ -1534,7 +1592,7 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
   out[i] = r;
 }
 
-#if SAIL_PHASE_TIMING
+#if SAIL_PHASE_TIMING || SAIL_CULL_STATS
 // phase-timing readout for the variant harness (tools/variant_bench.py --phases)
 extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
@@ -1552,6 +1610,10 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
   else if (A.kernelSet == SAIL_KSET_ROOM) hipLaunchKernelGGL(sail_trace_kernel_room, dim3(blocks), dim3(256), 0, s, A);
   else if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
   else hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(sail_accum_kernel, dim3(blocks), dim3(256), 0, s, A);
   return hipGetLastError();
 }
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s) {

@@ -319,3 +319,15 @@ def test_kernel_selection(gpu, fixtures):
         ctx.set_scene_dict(fixtures["scenes"][name])
         assert ctx.kernel_name() == k, name
         ctx.close()
+
+
+# ---- sample groups (small per-rank frames): staged samples added in order are bit-identical ---------------------
+@pytest.mark.parametrize("name", ["C1", "C3"])
+@pytest.mark.parametrize("groups", ["1", "2", "5"])
+@pytest.mark.parametrize("mode", [capi.ACCUM_SUM, capi.ACCUM_MIX])
+def test_sample_groups(gpu, fixtures, monkeypatch, name, groups, mode):
+    monkeypatch.setenv("SAIL_SAMPLE_GROUPS", groups)
+    got, want, st, segs, gaov, waov = _render_both(fixtures, name, 40, 24, 7, 5, mode=mode, aov=True, launch=7)
+    assert bit_equal(got, want).all()
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
