@@ -1088,17 +1088,30 @@ D void accumulateSample(float4& acc, V3 e, const SailSample& S, int mode) {
     acc.x = mx; acc.y = my; acc.z = mz; acc.w = 1.0f;
   }
 }
-// the workgroup's 16x16 block and sample range: blockIdx.x = group * (ownedTiles * 16) + block
-struct TileWork { int ownedTile, sub, kBeg, kEnd; long long slotBase; };
+// the workgroup's 16x16 block and sample range: blockIdx.x = group * (ownedTiles * 16) + block. Ungrouped
+// launches (one workgroup per block, every sample) are a separate compile-time instance, so they carry none of
+// the group bookkeeping in registers (sample groups add VGPR/SGPR spills to the flat kernels otherwise).
+struct TileWork { int ownedTile, sub, kBeg, kEnd, bid; };
+template <bool GROUPED>
 D TileWork tileWork(const SailTraceArgs& A) {
-  const int nb = A.ownedTiles * 16;
-  const int bid = (int)blockIdx.x % nb, group = (int)blockIdx.x / nb;
   TileWork w;
-  w.ownedTile = bid >> 4; w.sub = bid & 15;
-  w.kBeg = group * A.groupSpp;
-  w.kEnd = w.kBeg + A.groupSpp < A.spp ? w.kBeg + A.groupSpp : A.spp;
-  w.slotBase = (long long)bid * 256;
+  if (GROUPED) {
+    const int nb = A.ownedTiles * 16;
+    const int bid = (int)blockIdx.x % nb, group = (int)blockIdx.x / nb;
+    w.bid = bid;
+    w.kBeg = group * A.groupSpp;
+    w.kEnd = w.kBeg + A.groupSpp < A.spp ? w.kBeg + A.groupSpp : A.spp;
+  } else {
+    w.bid = (int)blockIdx.x;
+    w.kBeg = 0;
+    w.kEnd = A.spp;
+  }
+  w.ownedTile = w.bid >> 4; w.sub = w.bid & 15;
   return w;
+}
+// the staged radiance of sample k at lane li of block bid (stage row k, slot bid * 256 + li)
+D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
+  A.stage[(size_t)k * (size_t)A.stageStride + (size_t)bid * 256 + li] = make_float4(e.x, e.y, e.z, 0.0f);
 }
 
 }  // namespace
@@ -1108,9 +1121,9 @@ D TileWork tileWork(const SailTraceArgs& A) {
 #define SAIL_TRACE_MIN_WAVES 6
 #endif
 // CULL selects the padded-box pre-cull at compile time (two kernels), so small scenes carry none of its code.
-template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
 __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
-  const TileWork tw = tileWork(A);
+  const TileWork tw = tileWork<GROUPED>(A);
   const int ownedTile = tw.ownedTile;
   const int sub = tw.sub;
   const int tile = A.rank + ownedTile * A.world;
@@ -1146,7 +1159,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   const size_t pix = (size_t)y * A.W + x;
-  const bool grouped = A.sampleGroups > 1;
+  constexpr bool grouped = GROUPED;
   float4 acc = grouped ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : A.accum[pix];
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
@@ -1166,7 +1179,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     nAov = v3s(0.0f); pAov = v3s(0.0f);
     const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs, pc);
-    if (grouped) A.stage[(size_t)k * A.stageStride + tw.slotBase + threadIdx.x] = make_float4(e.x, e.y, e.z, 0.0f);
+    if (grouped) stageSample(A, k, tw.bid, threadIdx.x, e);
     else accumulateSample(acc, e, S, A.accumMode);
   }
   if (!grouped) A.accum[pix] = acc;
@@ -1199,7 +1212,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_COMPACT
 #define SAIL_COMPACT 1
 #endif
-template <bool CULL, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
@@ -1207,7 +1220,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   __shared__ float sE[3][256];
   __shared__ int sCnt[kKeys];
   __shared__ int sStart[kKeys + 1];
-  const TileWork tw = tileWork(A);
+  const TileWork tw = tileWork<GROUPED>(A);
   const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
   const int sub = tw.sub;
@@ -1231,7 +1244,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (li < kKeys) sCnt[li] = 0;
   __syncthreads();
   const size_t pixG = (size_t)y * A.W + x;
-  const bool grouped = A.sampleGroups > 1;
+  constexpr bool grouped = GROUPED;
   float4 acc = (valid && !grouped) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
@@ -1333,7 +1346,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     __syncthreads();
     if (valid) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
-      if (grouped) A.stage[(size_t)k * A.stageStride + tw.slotBase + li] = make_float4(er.x, er.y, er.z, 0.0f);
+      if (grouped) stageSample(A, k, tw.bid, li, er);
       else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
@@ -1357,16 +1370,23 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #define SAIL_TILE_SMALL traceTile
 #endif
 
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_MIN_WAVES) sail_trace_kernel(SailTraceArgs A) {
-  traceTile<false, ~0u, ~0u, ~0u, ~0u>(A);
-}
+// each plugin set has an ungrouped kernel (one workgroup per 16x16 block, every sample) and a _grouped one
+// (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel)
+#define SAIL_TRACE_KERNELS(name, waves, body, cull, ks, km, kt, kl)                                              \
+  extern "C" __global__ void __launch_bounds__(256, waves) name(SailTraceArgs A) {                               \
+    body<cull, false, ks, km, kt, kl>(A);                                                                        \
+  }                                                                                                              \
+  extern "C" __global__ void __launch_bounds__(256, waves) name##_grouped(SailTraceArgs A) {                     \
+    body<cull, true, ks, km, kt, kl>(A);                                                                         \
+  }
+
+SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, traceTile, false, ~0u, ~0u, ~0u, ~0u)
 // the README Cornell box plugin set (C1/C2/C5): Cube + Sphere + Cornellbox, Matte + Mirror, uniform colours
 #ifndef SAIL_TRACE_CORNELL_MIN_WAVES
 #define SAIL_TRACE_CORNELL_MIN_WAVES 7
 #endif
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CORNELL_MIN_WAVES) sail_trace_kernel_cornell(SailTraceArgs A) {
-  SAIL_TILE_SMALL<false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS>(A);
-}
+SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, false,
+                   SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS)
 // the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
@@ -1377,12 +1397,9 @@ extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CORNELL_MIN_WAVES) 
 #ifndef SAIL_ROOM_TILE
 #define SAIL_ROOM_TILE traceTile
 #endif
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_ROOM_MIN_WAVES) sail_trace_kernel_room(SailTraceArgs A) {
-  SAIL_ROOM_TILE<false, SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS>(A);
-}
-extern "C" __global__ void __launch_bounds__(256, SAIL_TRACE_CULL_MIN_WAVES) sail_trace_kernel_cull(SailTraceArgs A) {
-  traceTile<true, ~0u, ~0u, ~0u, ~0u>(A);
-}
+SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, false,
+                   SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS)
+SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, traceTile, true, ~0u, ~0u, ~0u, ~0u)
 
 // ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
 extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {
@@ -1606,10 +1623,13 @@ extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
 
 // ---- host launch wrappers (called by sail_capi.cpp) ----------------------------------------------------------------
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
-  if (A.kernelSet == SAIL_KSET_CORNELL) hipLaunchKernelGGL(sail_trace_kernel_cornell, dim3(blocks), dim3(256), 0, s, A);
-  else if (A.kernelSet == SAIL_KSET_ROOM) hipLaunchKernelGGL(sail_trace_kernel_room, dim3(blocks), dim3(256), 0, s, A);
-  else if (A.cullPrims) hipLaunchKernelGGL(sail_trace_kernel_cull, dim3(blocks), dim3(256), 0, s, A);
-  else hipLaunchKernelGGL(sail_trace_kernel, dim3(blocks), dim3(256), 0, s, A);
+  const bool g = A.sampleGroups > 1;
+#define SAIL_LAUNCH(k) hipLaunchKernelGGL(g ? k##_grouped : k, dim3(blocks), dim3(256), 0, s, A)
+  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH(sail_trace_kernel_cornell);
+  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH(sail_trace_kernel_room);
+  else if (A.cullPrims) SAIL_LAUNCH(sail_trace_kernel_cull);
+  else SAIL_LAUNCH(sail_trace_kernel);
+#undef SAIL_LAUNCH
   return hipGetLastError();
 }
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s) {
