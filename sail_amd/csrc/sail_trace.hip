@@ -178,9 +178,20 @@ struct Ctx {
 };
 #define HAS(set, id) (((set) >> (id)) & 1u)
 
+// Scene rows are read through the constant address space: the kernels also store to global memory (AOVs,
+// stage, accumulator) through pointers the compiler cannot prove disjoint from the scene, and without this
+// a wave-uniform primitive read becomes a per-lane vector load (VGPRs + TA cycles) instead of a scalar load.
+template <typename T> using ConstAS = const __attribute__((address_space(4))) T;
+template <typename T> D const T& constRow(const T* base, int i) { return *(const T*)((ConstAS<T>*)base + i); }
+#if SAIL_PRIMS_LDS
+#define PRIM(c, i) ((c).prims[i])
+#else
+#define PRIM(c, i) constRow<SailPrim>((c).prims, (i))
+#endif
+
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
-D float TP(const Ctx& c, int row, int col) { return c.tp[row * 16 + col]; }
-D V3 TP3(const Ctx& c, int row, int col) { return v3(c.tp[row * 16 + col], c.tp[row * 16 + col + 1], c.tp[row * 16 + col + 2]); }
+D float TP(const Ctx& c, int row, int col) { return constRow<float>(c.tp, row * 16 + col); }
+D V3 TP3(const Ctx& c, int row, int col) { return v3(TP(c, row, col), TP(c, row, col + 1), TP(c, row, col + 2)); }
 
 // ---- random.glsl:5-18 ---------------------------------------------------------------------------------
 D float hash1(const Ctx& c, float seed, float a, float b, float cc) {
@@ -333,11 +344,19 @@ D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
   else h.sc = v3s(0.0f);
 }
 
+// The quadrics' bounding-box test (testBoundboxFor*) and their root search are both pure predicates on the
+// ray, so their order is free: the discriminant rejects most rays more cheaply than the six-divide slab test,
+// and only candidate hits pay the exact slab test (same results; C3 +4 %, C4 +5 %, measured).
+#ifndef SAIL_BOX_LAST
+#define SAIL_BOX_LAST 1
+#endif
 // ---- sphere.glsl:45-86 ---------------------------------------------------------------------------------------
 D float sphereT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 c = P3(p, 0);
   const float rad = p.a[3];
+#if !SAIL_BOX_LAST
   if (!testBoundbox(r0, c - v3s(rad), c + v3s(rad))) return kMaxDistance;
+#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - c);
   const float a = dot(d, d), b = 2.0f * dot(o, d), cc = dot(o, o) - rad * rad;
   float t1 = 0.0f, t2 = 0.0f;
@@ -346,6 +365,9 @@ D float sphereT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   float t = t1;
   if (t1 < kEps) t = t2;
   if (t >= kMaxDistance) return kMaxDistance;
+#if SAIL_BOX_LAST
+  if (!testBoundbox(r0, c - v3s(rad), c + v3s(rad))) return kMaxDistance;
+#endif
   if (hitOut) *hitOut = o + t * d;
   return t;
 }
@@ -428,7 +450,9 @@ D bool rootPick(float t1, float t2, V3 o, V3 d, float zlo, float zhi, bool epsLo
 D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float h = p.a[3], rad = p.a[4];
+#if !SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float k = p.a[5];  // (rad / h)^2, per scene
   const float a = d.x * d.x + d.y * d.y - k * d.z * d.z;
@@ -438,13 +462,18 @@ D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
+#if SAIL_BOX_LAST
+  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
 D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float h = p.a[3], rad = p.a[4];
+#if !SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float a = d.x * d.x + d.y * d.y;
   const float b = 2.0f * (d.x * o.x + d.y * o.y);
@@ -453,16 +482,21 @@ D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
+#if SAIL_BOX_LAST
+  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
+#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
 D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float ah = p.a[9], ch = p.a[10];
+#if !SAIL_BOX_LAST
   {  // testBoundboxForHyperboloid :13-24 (rMax, zMin, zMax per scene)
     const float rMax = p.a[11], zMin = p.a[12], zMax = p.a[13];
     if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
   }
+#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float a = ah * d.x * d.x + ah * d.y * d.y - ch * d.z * d.z;
   const float b = 2.0f * (ah * d.x * o.x + ah * d.y * o.y - ch * d.z * o.z);
@@ -472,6 +506,12 @@ D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (t2 < -kEps) return kMaxDistance;
   const float zMin = p.a[12], zMax = p.a[13];
   if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
+#if SAIL_BOX_LAST
+  {  // testBoundboxForHyperboloid :13-24 (rMax, zMin, zMax per scene)
+    const float rMax = p.a[11], zMin = p.a[12], zMax = p.a[13];
+    if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
+  }
+#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
@@ -479,7 +519,9 @@ D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float z0 = p.a[3], z1 = p.a[4], rad = p.a[5];
   const float zMin = fmin_(z0, z1), zMax = fmax_(z0, z1);
+#if !SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
+#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float k = p.a[6];  // zMax / (rad * rad), per scene
   const float a = k * (d.x * d.x + d.y * d.y);
@@ -489,6 +531,9 @@ D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
+#if SAIL_BOX_LAST
+  if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
+#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
@@ -620,8 +665,8 @@ D void cullStat(bool pass) {
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !CULL_TEST(c, c.prims[i], r, best)) continue;
-    const float t = primT(c, c.prims[i], r, nullptr);
+    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
+    const float t = primT(c, PRIM(c, i), r, nullptr);
     if (t < best) {
       best = t;
       if (c.shadowAnyHit && best > kEps && best < kOneMinusEps) break;  // exact: no prim returns t <= EPSILON
@@ -639,17 +684,17 @@ D Sweep sweepRay(const Ctx& c, const Ray& r) {
   V3 bhl = v3s(0.0f);
 #if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !CULL_TEST(c, c.prims[i], r, best)) continue;
+    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
     V3 hl = v3s(0.0f);
-    const float t = primT(c, c.prims[i], r, &hl);
+    const float t = primT(c, PRIM(c, i), r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
   }
 #else
   for (int i = 0; i < c.n; i++) {
-    const float t = primT(c, c.prims[i], r, nullptr);
+    const float t = primT(c, PRIM(c, i), r, nullptr);
     if (t < best) { best = t; bi = i; }
   }
-  if (bi >= 0) primT(c, c.prims[bi], r, &bhl);  // the same arithmetic again, for the winner only
+  if (bi >= 0) primT(c, PRIM(c, bi), r, &bhl);  // the same arithmetic again, for the winner only
 #endif
   Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
   return sw;
@@ -663,7 +708,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
   h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0;
   if (bi < 0) return h;
-  const SailPrim& p = c.prims[bi];
+  const SailPrim& p = PRIM(c, bi);
   switch (p.type) {
     case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) cubeHit(c, p, r, best, h); break;
     case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) sphereHit(c, p, bhl, h); break;
@@ -695,7 +740,7 @@ D Hit intersectObjects(const Ctx& c, const Ray& r, PhaseClock& pc) {
 D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
   normal = v3s(0.0f);
   pdf = 0.0f;
-  const SailPrim& p = c.prims[row];
+  const SailPrim& p = PRIM(c, row);
   const float s = sgn(p.rev);
   switch (p.type) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
@@ -1173,7 +1218,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
-    const SailSample& S = A.samples[k];
+    const SailSample& S = constRow<SailSample>(A.samples, k);
     const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
     const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
@@ -1256,7 +1301,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
-    const SailSample& S = A.samples[k];
+    const SailSample& S = constRow<SailSample>(A.samples, k);
     const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
     bool alive = valid;
     int pixel = li;
@@ -1285,7 +1330,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           }
           alive = false;
         } else {
-          const SailPrim& p = c.prims[sw.bi];
+          const SailPrim& p = PRIM(c, sw.bi);
           int mc = to_int(TP(c, p.matRow, 0));
           mc = (mc >= 0 && mc < 5) ? mc : 0;
           key = 1 + p.type * 5 + mc;
@@ -1415,7 +1460,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArg
   const float4* st = A.stage + (long long)bid * 256 + li;
   for (int k = 0; k < A.spp; k++) {
     const float4 v = st[(size_t)k * A.stageStride];
-    accumulateSample(acc, v3(v.x, v.y, v.z), A.samples[k], A.accumMode);
+    accumulateSample(acc, v3(v.x, v.y, v.z), constRow<SailSample>(A.samples, k), A.accumMode);
   }
   A.accum[pix] = acc;
 }
@@ -1578,7 +1623,7 @@ extern "C" __global__ void __launch_bounds__(64) sail_pick_kernel(const SailPrim
   float best = kMaxDistance;
   int bi = -1;
   for (int k = 0; k < n; k++) {
-    const float t = primT(c, prims[k], r, nullptr);
+    const float t = primT(c, constRow<SailPrim>(prims, k), r, nullptr);
     if (t < best) { best = t; bi = k; }
   }
   index[i] = bi;
