@@ -107,6 +107,7 @@ struct sail_ctx {
   sail_plugins plugins{};
   bool haveScene = false;
   int shadowAnyHit = 0;
+  std::vector<unsigned long long> typeMasksHost;  // staging for the per-chunk type masks (async copy source)
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
@@ -419,7 +420,8 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
     SailTraceArgs A;
     memset(&A, 0, sizeof A);
-    A.prims = c->prims; A.texparams = c->tp; A.lights = c->lt; A.lightObjRow = c->lightObjRow;
+    A.prims = c->prims; A.typeMasks = reinterpret_cast<const unsigned long long*>(c->prims + c->n);
+    A.texparams = c->tp; A.lights = c->lt; A.lightObjRow = c->lightObjRow;
     A.samples = c->samples + s0;
     A.accum = c->accum; A.aovN = c->aovN; A.aovP = c->aovP; A.segCounter = c->segCounter;
     A.W = c->W; A.H = c->H; A.n = c->n; A.tn = c->tn; A.ln = c->ln;
@@ -554,6 +556,25 @@ void sail_destroy(sail_ctx* c) {
   delete c;
 }
 
+// The primitive buffer holds the decoded rows followed by the candidate sweep's per-type masks: for each chunk
+// of 64 rows, 16 words whose bit j says row 64*chunk + j has shape type t (SailTraceArgs.typeMasks).
+static size_t primBytes(int n) {
+  const size_t chunks = (size_t)(n + 63) / 64;
+  return sizeof(SailPrim) * (size_t)(n > 0 ? n : 1) + chunks * 16 * sizeof(unsigned long long);
+}
+static int uploadPrims(sail_ctx* c, const std::vector<SailPrim>& prims) {
+  const int n = (int)prims.size();
+  if (n <= 0) return SAIL_OK;
+  const size_t chunks = (size_t)(n + 63) / 64;
+  c->typeMasksHost.assign(chunks * 16, 0ull);
+  for (int i = 0; i < n; i++)
+    if (prims[i].type >= 0 && prims[i].type < 16) c->typeMasksHost[(size_t)(i / 64) * 16 + prims[i].type] |= 1ull << (i % 64);
+  HIPCHK(c, hipMemcpyAsync(c->prims, prims.data(), sizeof(SailPrim) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->prims + n, c->typeMasksHost.data(), chunks * 16 * sizeof(unsigned long long),
+                           hipMemcpyHostToDevice, c->stream));
+  return SAIL_OK;
+}
+
 int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texparams, int tn, const float* lights,
                    int ln, const sail_plugins* plugins) {
   if (!c) return SAIL_E_INVALID;
@@ -576,14 +597,14 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   void* old[] = {c->prims, c->tp, c->lt, c->lightObjRow};
   for (void* b : old) if (b) HIPCHK(c, hipFree(b));
   c->prims = nullptr; c->tp = nullptr; c->lt = nullptr; c->lightObjRow = nullptr;
-  const size_t pb = sizeof(SailPrim) * (size_t)(n > 0 ? n : 1), tb = sizeof(float) * 16 * (size_t)(tn > 0 ? tn : 1),
+  const size_t pb = primBytes(n), tb = sizeof(float) * 16 * (size_t)(tn > 0 ? tn : 1),
                lb = sizeof(float) * 18 * (size_t)(ln > 0 ? ln : 1), rb = sizeof(int32_t) * lrow.size();
   if (hipMalloc(&c->prims, pb) != hipSuccess || hipMalloc(&c->tp, tb) != hipSuccess || hipMalloc(&c->lt, lb) != hipSuccess ||
       hipMalloc(&c->lightObjRow, rb) != hipSuccess)
     return fail(c, SAIL_E_OOM, "scene buffers");
   HIPCHK(c, hipMemsetAsync(c->tp, 0, tb, c->stream));
   HIPCHK(c, hipMemsetAsync(c->lt, 0, lb, c->stream));
-  if (n > 0) HIPCHK(c, hipMemcpyAsync(c->prims, prims.data(), sizeof(SailPrim) * n, hipMemcpyHostToDevice, c->stream));
+  if (int rc = uploadPrims(c, prims)) return rc;
   if (tn > 0) HIPCHK(c, hipMemcpyAsync(c->tp, texparams, sizeof(float) * 16 * tn, hipMemcpyHostToDevice, c->stream));
   if (ln > 0) HIPCHK(c, hipMemcpyAsync(c->lt, lights, sizeof(float) * 18 * ln, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->lightObjRow, lrow.data(), rb, hipMemcpyHostToDevice, c->stream));
@@ -601,7 +622,8 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   std::vector<SailPrim> prims;
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit);
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (n > 0) HIPCHK(c, hipMemcpyAsync(c->prims, prims.data(), sizeof(SailPrim) * n, hipMemcpyHostToDevice, c->stream));
+  if (int rc = uploadPrims(c, prims)) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->objectsRows.assign(objects, objects + (size_t)n * 18);
   return resetAccum(c);
 }

@@ -40,6 +40,7 @@ struct __attribute__((aligned(16))) SailSample {
 
 struct SailTraceArgs {
   const SailPrim* prims;
+  const unsigned long long* typeMasks;  // per 64-row chunk: 16 words, bit j of word t = row 64*chunk+j has type t
   const float* texparams;   // tn x 16
   const float* lights;      // ln x 18
   const int32_t* lightObjRow;  // per light row: decoded object row of the area-light geometry

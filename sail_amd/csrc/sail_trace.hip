@@ -166,6 +166,7 @@ struct Hit {
 };
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
+  const unsigned long long* typeMasks;
   int n, tn, ln;
   uint32_t matMask, texMask, lightMask;
   float fcx, fcy;
@@ -661,11 +662,85 @@ D void cullStat(bool pass) {
 #define CULL_TEST(c, p, r, best) padHit(p, r, best)
 #endif
 
-// closest distance only (shadow rays, testShadow shader.light.js:24-31)
+// ---- candidate sweep (pre-cull kernel) ----------------------------------------------------------------------
+// In the uniform sweep a wave runs a primitive's exact test whenever any lane passes its pre-cull; on C4
+// (67 primitives, incoherent bounce rays) that is 35 % of the (wave, primitive) pairs with 4.7 of 53 lanes
+// passing. Here every lane first collects its candidates of a 64-row chunk into a bit mask (uniform pre-cull
+// loop, scalar row reads), then, one shape type at a time, each lane tests its own next candidate of that
+// type: the wave runs max-over-lanes iterations instead of one per primitive any lane needs. Candidates are
+// visited out of row order, so a hit replaces the best one when it is nearer, or equally near with a lower
+// row -- the winner of the in-order "t < best" sweep. Pre-culled rows cannot win (padHit), nor tie.
+#ifndef SAIL_CAND_SWEEP
+#define SAIL_CAND_SWEEP 1
+#endif
+#ifndef SAIL_CAND_RECULL
+#define SAIL_CAND_RECULL 0
+#endif
+template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
+  if constexpr (T == SAIL_CUBE) return cubeT(p, r);
+  else if constexpr (T == SAIL_SPHERE) return sphereT(p, r, hl);
+  else if constexpr (T == SAIL_RECTANGLE) return rectT(p, r, hl);
+  else if constexpr (T == SAIL_CONE) return coneT(p, r, hl);
+  else if constexpr (T == SAIL_CYLINDER) return cylinderT(p, r, hl);
+  else if constexpr (T == SAIL_DISK) return diskT(p, r, hl);
+  else if constexpr (T == SAIL_HYPERBOLOID) return hypT(p, r, hl);
+  else if constexpr (T == SAIL_PARABOLOID) return paraT(p, r, hl);
+  else if constexpr (T == SAIL_CORNELLBOX) return cornellT(p, r);
+  else return kMaxDistance;
+}
+template <int T>
+D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
+  if (!HAS(c.kShapes, T)) return;
+  unsigned long long m = cand & constRow<unsigned long long>(c.typeMasks, (base >> 6) * 16 + T);
+  while (__ballot(m != 0ull)) {
+    if (m != 0ull) {
+      const int i = base + __builtin_ctzll(m);
+      m &= m - 1ull;
+      const SailPrim& p = PRIM(c, i);
+#if SAIL_CAND_RECULL
+      if (!padHit(p, r, best)) continue;
+#endif
+      V3 hl = v3s(0.0f);
+      const float t = typedT<T>(p, r, &hl);
+      if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
+    }
+  }
+}
+// limit: the pre-cull distance bound before any hit (kMaxDistance, or 1 for shadow rays: see closestT)
+D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, V3& bhl) {
+  for (int base = 0; base < c.n; base += 64) {
+    const int cnt = c.n - base < 64 ? c.n - base : 64;
+    const float bound = fmin_(best, limit);
+    unsigned long long cand = 0ull;
+    for (int j = 0; j < cnt; j++)
+      if (CULL_TEST(c, PRIM(c, base + j), r, bound)) cand |= 1ull << j;
+    candType<SAIL_CUBE>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CORNELLBOX>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_RECTANGLE>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_DISK>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_SPHERE>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CYLINDER>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CONE>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_PARABOLOID>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_HYPERBOLOID>(c, r, base, cand, best, bi, bhl);
+  }
+}
+
+// closest distance only (shadow rays, testShadow shader.light.js:24-31). The caller only asks whether the
+// closest distance lies in (EPSILON, 1 - EPSILON): a primitive whose padded box starts beyond 1 cannot change
+// that answer (if it were the closest, every distance would be >= 1 - EPSILON), so the pre-cull bound
+// starts at 1 instead of MAX_DISTANCE. Returned distances beyond that bound are not exact.
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
+#if SAIL_CAND_SWEEP
+  if (c.cullPrims && !c.shadowAnyHit) {
+    int bi = -1; V3 bhl = v3s(0.0f);
+    candSweep(c, r, 1.0f, best, bi, bhl);
+    return best;
+  }
+#endif
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
+    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, fmin_(best, 1.0f))) continue;
     const float t = primT(c, PRIM(c, i), r, nullptr);
     if (t < best) {
       best = t;
@@ -682,6 +757,13 @@ D Sweep sweepRay(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
   int bi = -1;
   V3 bhl = v3s(0.0f);
+#if SAIL_CAND_SWEEP
+  if (c.cullPrims) {
+    candSweep(c, r, kMaxDistance, best, bi, bhl);
+    Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
+    return sw;
+  }
+#endif
 #if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
     if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
@@ -1190,7 +1272,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   if (x >= A.W || y >= A.H || ownedTile >= A.ownedTiles) return;
 
   Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
 #if SAIL_PRIMS_LDS
   c.prims = sPrims;
 #else
@@ -1277,7 +1359,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   const bool valid = x < A.W && y < A.H;   // ragged tiles: invalid lanes still serve migrated paths
 
   Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
   c.prims = A.prims;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
@@ -1434,7 +1516,7 @@ SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL
                    SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS)
 // the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
-#define SAIL_TRACE_CULL_MIN_WAVES 8
+#define SAIL_TRACE_CULL_MIN_WAVES 7
 #endif
 #ifndef SAIL_TRACE_ROOM_MIN_WAVES
 #define SAIL_TRACE_ROOM_MIN_WAVES 6
@@ -1442,7 +1524,10 @@ SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL
 #ifndef SAIL_ROOM_TILE
 #define SAIL_ROOM_TILE traceTile
 #endif
-SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, false,
+#ifndef SAIL_ROOM_CULL
+#define SAIL_ROOM_CULL false
+#endif
+SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
                    SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS)
 SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, traceTile, true, ~0u, ~0u, ~0u, ~0u)
 

@@ -301,6 +301,21 @@ def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, 
     assert st.segments == segs
 
 
+# ---- candidate sweep (pre-cull kernel): rows span three 64-row chunks, and every row has an identical twin,
+# so equal distances from different rows are everywhere: the lower row must win, as in the in-order sweep ------
+@pytest.mark.parametrize("cull", ["0", "1000"])
+def test_candidate_sweep_chunks_and_ties(gpu, fixtures, monkeypatch, cull):
+    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+    sc = dict(fixtures["scenes"]["C4"])
+    sc["objects"] = list(sc["objects"]) * 2
+    sc["n"] = 2 * sc["n"]                       # 134 rows: chunks of 64, 64, 6
+    fixtures = {"scenes": {"C4x2": sc}}
+    got, want, st, segs, gaov, waov = _render_both(fixtures, "C4x2", 24, 16, 2, 8, aov=True, launch=2)
+    assert bit_equal(got, want).all()
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
+
+
 # ---- plugin-set kernels: the Cornell-box kernel (C1 scenes by default) and the generic one agree bit for bit --
 @pytest.mark.parametrize("force", ["0", "1"])
 def test_plugin_set_kernels(gpu, fixtures, monkeypatch, force):
