@@ -1152,15 +1152,26 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
 
 // ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
 D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc);
-D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, V3& n, V3& p, unsigned& segs, PhaseClock& pc) {
+// fstrace.glsl:15-16 AOVs (normal/2 + 0.5, normalize(p)) of the first hit; a primary miss stores n = p = 0
+D void storeAov(float4* aovN, float4* aovP, size_t g, V3 n, V3 p) {
+  const V3 qn = n / 2.0f + 0.5f, qp = normalize(p);
+  if (aovN) aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+  if (aovP) aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+}
+// aovPix >= 0: this sample's first hit is stored as the pixel's AOVs (written at once, not carried in registers)
+D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, float4* aovN, float4* aovP, long long aovPix,
+           unsigned& segs, PhaseClock& pc) {
   V3 fpdf = v3s(1.0f), e = v3s(0.0f);
   for (int depth = 1; depth <= maxDepth; depth++) {
     segs++;
     const Hit ins = intersectObjects(c, ray, pc);
     PHASE_MARK(pc, 1);  // hit record of the winner
     const float seed = tss + (float)depth;
+    if (depth == 1 && aovPix >= 0) {
+      const bool hit = ins.d < kMaxDistance;
+      storeAov(aovN, aovP, (size_t)aovPix, hit ? ins.normal : v3s(0.0f), hit ? ins.hit : v3s(0.0f));
+    }
     if (ins.d >= kMaxDistance) break;
-    if (depth == 1) { n = ins.normal; p = ins.hit; }
     shadeBounce(c, ins, ray, seed, fpdf, e, pc);
   }
   return e;
@@ -1287,12 +1298,15 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 
   const size_t pix = (size_t)y * A.W + x;
   constexpr bool grouped = GROUPED;
-  float4 acc = grouped ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : A.accum[pix];
-  const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
-  const bool tri0 = s + t <= 1.0f;
-  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
+  // per-pixel state that is only touched once per sample lives in LDS, not in registers across the bounces
+  // (the pre-cull kernel is register-bound: every freed VGPR is spill traffic saved)
+  __shared__ float4 sAcc[256];
+  __shared__ float2 sST[256];
+  const int li = threadIdx.x;
+  sAcc[li] = grouped ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : A.accum[pix];
+  sST[li] = make_float2(((float)x + 0.5f) / (float)A.W, ((float)y + 0.5f) / (float)A.H);
   const bool aovGroup = tw.kEnd == A.spp;  // the group holding the launch's last sample writes the AOVs
-  V3 nAov = v3s(0.0f), pAov = v3s(0.0f);
+  const bool wantAov = (A.aovN || A.aovP) && aovGroup;
   unsigned segs = 0;
   PhaseClock pc;
 #if SAIL_PHASE_TIMING
@@ -1301,23 +1315,18 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #endif
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = constRow<SailSample>(A.samples, k);
+    const float s = sST[li].x, t = sST[li].y;
+    const bool tri0 = s + t <= 1.0f;
+    const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
     const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
     const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
-    nAov = v3s(0.0f); pAov = v3s(0.0f);
-    const V3 e = trace(c, ray, S.seed, A.maxBounces, nAov, pAov, segs, pc);
+    const long long aovPix = (wantAov && k == A.spp - 1) ? (long long)pix : -1;
+    const V3 e = trace(c, ray, S.seed, A.maxBounces, A.aovN, A.aovP, aovPix, segs, pc);
     if (grouped) stageSample(A, k, tw.bid, threadIdx.x, e);
-    else accumulateSample(acc, e, S, A.accumMode);
+    else { float4 acc = sAcc[li]; accumulateSample(acc, e, S, A.accumMode); sAcc[li] = acc; }
   }
-  if (!grouped) A.accum[pix] = acc;
-  if (A.aovN && aovGroup) {
-    const V3 q = nAov / 2.0f + 0.5f;
-    A.aovN[pix] = make_float4(q.x, q.y, q.z, 1.0f);
-  }
-  if (A.aovP && aovGroup) {
-    const V3 q = normalize(pAov);
-    A.aovP[pix] = make_float4(q.x, q.y, q.z, 1.0f);
-  }
+  if (!grouped) A.accum[pix] = sAcc[li];
 #if SAIL_PHASE_TIMING
   PHASE_MARK(pc, 7);  // accumulate + store
   if (lane == 0)
@@ -1512,7 +1521,10 @@ SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, traceTile, false, ~0
 #ifndef SAIL_TRACE_CORNELL_MIN_WAVES
 #define SAIL_TRACE_CORNELL_MIN_WAVES 7
 #endif
-SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, false,
+#ifndef SAIL_CORNELL_CULL
+#define SAIL_CORNELL_CULL false
+#endif
+SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
                    SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS)
 // the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
