@@ -211,8 +211,11 @@ def test_filter_bit_exact(gpu, fixtures, kind, fname, r, gamma):
     assert (got8[..., :3] == want8).all()
 
 
-def test_update_objects_and_reset(gpu, fixtures):
-    """Tracer.updateObjects path (tracer.js:25-40): new rows, accumulation restarts."""
+@pytest.mark.parametrize("cull", ["0", "1000"])
+def test_update_objects_and_reset(gpu, fixtures, monkeypatch, cull):
+    """Tracer.updateObjects path (tracer.js:25-40): new rows, accumulation restarts (with the pre-cull kernel
+    forced on, the candidate sweep's per-chunk type masks are re-uploaded with the rows)."""
+    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
     sc = fixtures["scenes"]["C1"]
     W, H = 32, 32
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, 2)
