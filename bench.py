@@ -39,6 +39,7 @@ CONFIGS = {
 CONFIG = CONFIGS["C2"]
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
+VALU_CLOCK_HZ = 2.4e9      # MI355X peak engine clock, if the device does not report one
 
 
 def load_scene(name="C1"):
@@ -132,8 +133,24 @@ def profiled_traffic(workload, px, spp, bounces):
             rec = json.load(f)
         L = rec.get("launch", {})
         if rec.get("workload", "cornell_box_readme_C2") == workload and L.get("pixels") == px and L.get("spp") == spp and L.get("bounces") == bounces:
-            return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+            return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT), rec
+    return None, None, None
+
+
+def valu_issue(pmc, avg_launch_s, device):
+    """Executed wave64 VALU instructions per launch (PMC SQ_INSTS_VALU, the same committed summary as
+    `traffic`) per second of the live launch time, against one wave64 VALU issue per SIMD every 2 cycles
+    (v_fma_f32 throughput, MI355X_MICROARCH.md) at the device's peak engine clock: how busy the vector pipe is,
+    as opposed to the algorithmic-op fraction above (f64 and transcendental instructions take 4-8 cycles,
+    so this understates the pipe's occupancy)."""
+    if not pmc or "SQ_INSTS_VALU" not in pmc.get("sq", {}):
+        return None
+    cus, clock = capi.device_info(device)
+    clock = clock if clock > 0 else VALU_CLOCK_HZ
+    peak = cus * 4 * clock / 2
+    achieved = pmc["sq"]["SQ_INSTS_VALU"] / avg_launch_s
+    return {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1), "unit": "G wave-instr/s",
+            "frac": round(achieved / peak, 4), "lane_utilisation": round(pmc.get("derived", {}).get("valu_lane_utilisation", 0.0), 3)}
 
 
 def main():
@@ -232,7 +249,7 @@ def main():
         ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
-        traffic, traffic_src = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B)
+        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B)
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
@@ -257,6 +274,7 @@ def main():
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},
+                "valu_issue": valu_issue(pmc, avg_launch_s, local_rank),
             },
         }
         if flt:

@@ -76,6 +76,9 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
 void sail_destroy(sail_ctx* ctx);
 const char* sail_last_error(const sail_ctx* ctx); /* ctx may be NULL: last creation error */
 int sail_device_count(int* count);
+/* Device facts for reports (bench.py's roofline): compute units and peak engine clock in kHz. No reference
+ * counterpart (WebGL exposes neither). */
+int sail_device_info(int device, int* compute_units, int* clock_khz);
 
 /* Tracer.update(scene) (src/core/tracer.js:42-90): the objects / texParams / lights rows exactly as
  * gen() serialises them (18 / 16 / 18 floats per row, Appendix A of SURVEY.md). Copied. */

@@ -25,7 +25,7 @@ FILTER_WAVELET, FILTER_NORMAL, FILTER_POSITION = 4, 5, 6  # need FLAG_AOV
 
 # exported symbols (kept in sync with include/sail_hip.h; tests/test_capi_symbols.py checks both ways)
 EXPORTS = (
-    "sail_create", "sail_destroy", "sail_last_error", "sail_device_count", "sail_set_scene",
+    "sail_create", "sail_destroy", "sail_last_error", "sail_device_count", "sail_device_info", "sail_set_scene",
     "sail_update_objects", "sail_set_accum_mode", "sail_set_partition", "sail_set_launch_samples",
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
@@ -88,6 +88,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_destroy": (None, [vp]),
         "sail_last_error": (ctypes.c_char_p, [vp]),
         "sail_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "sail_device_info": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
         "sail_set_scene": (ctypes.c_int, [vp, f32p, ctypes.c_int, f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.POINTER(Plugins)]),
         "sail_update_objects": (ctypes.c_int, [vp, f32p, ctypes.c_int]),
         "sail_set_accum_mode": (ctypes.c_int, [vp, ctypes.c_int]),
@@ -196,6 +197,15 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     lib.sail_device_count(ctypes.byref(n))
     return n.value
+
+
+def device_info(device: int = 0):
+    """(compute units, peak engine clock in Hz) of a device."""
+    lib = load()
+    cus, khz = ctypes.c_int(0), ctypes.c_int(0)
+    if lib.sail_device_info(device, ctypes.byref(cus), ctypes.byref(khz)) != 0:
+        raise SailError(f"sail_device_info({device}) failed")
+    return cus.value, khz.value * 1e3
 
 
 def comm_unique_id() -> bytes:

@@ -503,6 +503,17 @@ int sail_device_count(int* count) {
   return SAIL_OK;
 }
 
+int sail_device_info(int device, int* compute_units, int* clock_khz) {
+  if (!compute_units || !clock_khz) return SAIL_E_INVALID;
+  int cus = 0, khz = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, device) != hipSuccess)
+    return SAIL_E_HIP;
+  *compute_units = cus;
+  *clock_khz = khz;
+  return SAIL_OK;
+}
+
 const char* sail_last_error(const sail_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flags) {

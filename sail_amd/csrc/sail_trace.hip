@@ -1498,8 +1498,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if (lane == 0) atomicAdd(A.segCounter, v);
   }
 }
-// Compaction pays where shading diverges and the sweep is short (the Cornell kernel: C2 +6 %); in the generic
-// and pre-cull kernels its extra live state costs more in spills than it saves (C3 -4 %, C4 -14 %, measured).
+// Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;
+// earlier builds with more live state lost to spills in the flat kernels). SAIL_COMPACT=0 / SAIL_*_TILE select
+// the unsorted body for comparisons.
 #if SAIL_COMPACT
 #define SAIL_TILE_SMALL traceTileCompact
 #else
@@ -1516,7 +1517,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     body<cull, true, ks, km, kt, kl>(A);                                                                         \
   }
 
-SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, traceTile, false, ~0u, ~0u, ~0u, ~0u)
+#ifndef SAIL_GENERIC_TILE
+#define SAIL_GENERIC_TILE SAIL_TILE_SMALL
+#endif
+SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, SAIL_GENERIC_TILE, false, ~0u, ~0u, ~0u, ~0u)
 // the README Cornell box plugin set (C1/C2/C5): Cube + Sphere + Cornellbox, Matte + Mirror, uniform colours
 #ifndef SAIL_TRACE_CORNELL_MIN_WAVES
 #define SAIL_TRACE_CORNELL_MIN_WAVES 7
@@ -1526,22 +1530,26 @@ SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, traceTile, false, ~0
 #endif
 SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
                    SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS)
-// the pre-cull kernel serves scenes with many primitives, whose divergent shading prefers more waves (C4: 8)
-#ifndef SAIL_TRACE_CULL_MIN_WAVES
-#define SAIL_TRACE_CULL_MIN_WAVES 7
-#endif
+// rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
 #ifndef SAIL_TRACE_ROOM_MIN_WAVES
-#define SAIL_TRACE_ROOM_MIN_WAVES 6
+#define SAIL_TRACE_ROOM_MIN_WAVES 7
 #endif
 #ifndef SAIL_ROOM_TILE
-#define SAIL_ROOM_TILE traceTile
+#define SAIL_ROOM_TILE SAIL_TILE_SMALL
 #endif
 #ifndef SAIL_ROOM_CULL
 #define SAIL_ROOM_CULL false
 #endif
 SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
                    SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS)
-SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, traceTile, true, ~0u, ~0u, ~0u, ~0u)
+// the pre-cull kernel serves scenes with many primitives (C4: 7 waves measured best of 5-8)
+#ifndef SAIL_TRACE_CULL_MIN_WAVES
+#define SAIL_TRACE_CULL_MIN_WAVES 7
+#endif
+#ifndef SAIL_CULL_TILE
+#define SAIL_CULL_TILE SAIL_TILE_SMALL
+#endif
+SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u)
 
 // ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
 extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {
