@@ -12,6 +12,11 @@
 //   min/max  -> IEEE-754-2019 minimumNumber/maximumNumber (NaN -> other operand, -0 < +0), which is what
 //               GLSL min/max compile to on AMD GPUs (v_min_f32 / v_max_f32)
 //   sqrt     -> IEEE correctly-rounded f32 sqrt
+//   a / b    -> a * RN(1/b): the reciprocal-multiply form GPU shader compilers emit for GLSL division (GLSL ES
+//               3.00 §4.5.1 allows 2.5 ulp), with the reciprocal correctly rounded so that every implementation
+//               reproduces it (the MI355X sequence is checked against 1.0f/b for all 2^32 inputs,
+//               tools/rcp_probe.hip). Applies to every GLSL float division; the spec functions above keep
+//               their internal IEEE divides.
 //   int(x)   -> truncation, NaN -> 0, saturating
 #pragma once
 #include <stdint.h>
@@ -196,6 +201,8 @@ static inline float fmax_s(float a, float b) {
 static inline float floor_s(float x) { return floorf(x); }
 static inline float fract_s(float x) { return x - floorf(x); }
 static inline float sqrt_s(float x) { return sqrtf(x); }
+static inline float rcp_s(float b) { return 1.0f / b; }              // RN(1/b), IEEE
+static inline float div_s(float a, float b) { return a * rcp_s(b); }  // GLSL a / b
 static inline int to_int(float x) {
   if (x != x) return 0;
   if (x >= 2147483647.0f) return 2147483647;

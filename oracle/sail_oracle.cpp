@@ -25,9 +25,17 @@
 #include <math.h>
 #include "ref_math.h"
 
+// The scalar type of all GLSL arithmetic. A class (not a typedef of float) so that GLSL division has its
+// defined meaning a * RN(1/b) (ref_math.h div_s) everywhere; the SAIL_COUNT_OPS build also counts ops
+// (every + - * / min max sqrt and transcendental = 1, SURVEY §8(d) op model).
 #ifdef SAIL_COUNT_OPS
-// Op-counting scalar: every + - * / min max sqrt and transcendental counts 1 (SURVEY §8(d) op model).
 static unsigned long long g_ops = 0;
+#define OPINC() (g_ops++)
+#define OPC(k) (g_ops += (k))
+#else
+#define OPINC() ((void)0)
+#define OPC(k) ((void)0)
+#endif
 struct F {
   float v;
   F() : v(0.0f) {}
@@ -36,10 +44,10 @@ struct F {
   F(int x) : v((float)x) {}
   explicit operator float() const { return v; }
 };
-static inline F operator+(F a, F b) { g_ops++; return F(a.v + b.v); }
-static inline F operator-(F a, F b) { g_ops++; return F(a.v - b.v); }
-static inline F operator*(F a, F b) { g_ops++; return F(a.v * b.v); }
-static inline F operator/(F a, F b) { g_ops++; return F(a.v / b.v); }
+static inline F operator+(F a, F b) { OPINC(); return F(a.v + b.v); }
+static inline F operator-(F a, F b) { OPINC(); return F(a.v - b.v); }
+static inline F operator*(F a, F b) { OPINC(); return F(a.v * b.v); }
+static inline F operator/(F a, F b) { OPINC(); return F(refm::div_s(a.v, b.v)); }
 static inline F operator-(F a) { return F(-a.v); }
 static inline bool operator<(F a, F b) { return a.v < b.v; }
 static inline bool operator>(F a, F b) { return a.v > b.v; }
@@ -50,12 +58,7 @@ static inline bool operator!=(F a, F b) { return a.v != b.v; }
 static inline F& operator+=(F& a, F b) { a = a + b; return a; }
 static inline F& operator*=(F& a, F b) { a = a * b; return a; }
 static inline float raw(F a) { return a.v; }
-#define OPC(k) (g_ops += (k))
-#else
-typedef float F;
-static inline float raw(F a) { return a; }
-#define OPC(k) ((void)0)
-#endif
+static inline float fdiv_s(float a, float b) { return refm::div_s(a, b); }  // GLSL a / b on raw floats
 
 // ---- scalar builtins (GLSL semantics, ref_math.h spec) ----------------------------------------------
 static inline F fmin_(F a, F b) { OPC(1); return F(refm::fmin_s(raw(a), raw(b))); }
@@ -181,19 +184,19 @@ static inline F fetch(const Tex& t, float cx, float cy) {
   return F(t.d[texel(cy, t.h) * t.w + texel(cx, t.w)]);
 }
 // coordinate arithmetic is texture addressing, not shader arithmetic: kept in raw f32 (not counted)
-static inline F readFloat(const Tex& t, float x, F y, float width) { return fetch(t, x / width, raw(y)); }
+static inline F readFloat(const Tex& t, float x, F y, float width) { return fetch(t, fdiv_s(x, width), raw(y)); }
 static inline int readInt(const Tex& t, float x, F y, float width) { return toint(readFloat(t, x, y, width)); }
 static inline bool readBool(const Tex& t, float x, F y, float width) { return readInt(t, x, y, width) == 1; }
 static inline V3 readVec3(const Tex& t, float x, F y, float width) {
-  float px = x / width;
+  float px = fdiv_s(x, width);
   V3 r;
-  r.x = fetch(t, px, raw(y)); px += 1.0f / width;
-  r.y = fetch(t, px, raw(y)); px += 1.0f / width;
+  r.x = fetch(t, px, raw(y)); px += fdiv_s(1.0f, width);
+  r.y = fetch(t, px, raw(y)); px += fdiv_s(1.0f, width);
   r.z = fetch(t, px, raw(y));
   return r;
 }
-static inline F rowCoord(int i, int n) { return F((float)i / (float)(n - 1)); }  // float(i)/float(n-1)
-static inline F matCoord(F v) { return F(raw(v) / (float)(C.tn - 1)); }            // readFloat(...)/float(tn-1)
+static inline F rowCoord(int i, int n) { return F(fdiv_s((float)i, (float)(n - 1))); }  // float(i)/float(n-1)
+static inline F matCoord(F v) { return F(fdiv_s(raw(v), (float)(C.tn - 1))); }         // readFloat(...)/float(tn-1)
 
 // ---- struct.glsl:1-18 ------------------------------------------------------------------------------
 struct Intersect {
@@ -1220,7 +1223,7 @@ static void cornerDirs(const float* M, const float* eye, V3 out[4]) {
   for (int c = 0; c < 4; c++) {
     float q[4];
     for (int r = 0; r < 4; r++) q[r] = M[0 * 4 + r] * cx[c] + M[1 * 4 + r] * cy[c] + M[2 * 4 + r] * 0.0f + M[3 * 4 + r] * 1.0f;
-    const V3 w = v3(F(q[0] / q[3]), F(q[1] / q[3]), F(q[2] / q[3]));
+    const V3 w = v3(F(q[0]) / F(q[3]), F(q[1]) / F(q[3]), F(q[2]) / F(q[3]));  // ensure3byW, utility.glsl:11-13
     out[c] = normalize(w - v3(F(eye[0]), F(eye[1]), F(eye[2])));
   }
 }
@@ -1340,21 +1343,21 @@ int oracle_filter(const float* mean, int W, int H, int kind, const float* weight
         o[0] = col[0]; o[1] = col[1]; o[2] = col[2];
       } else if (kind == FILTER_GAMMA) {  // gamma.glsl:1-8
         bilinear(mean, W, H, tcx, tcy, col);
-        const float g = 1.0f / gamma_c;
+        const float g = fdiv_s(1.0f, gamma_c);
         o[0] = refm::pow_s(col[0], g); o[1] = refm::pow_s(col[1], g); o[2] = refm::pow_s(col[2], g);
       } else if (kind == FILTER_TONEMAP) {  // tonemapping.glsl:1-9
         bilinear(mean, W, H, tcx, tcy, col);
         for (int c = 0; c < 3; c++) {
           const float xx = refm::fmax_s(0.0f, col[c] - 0.004f);
-          o[c] = (xx * (6.2f * xx + 0.5f)) / (xx * (6.2f * xx + 1.7f) + 0.06f);
+          o[c] = fdiv_s(xx * (6.2f * xx + 0.5f), xx * (6.2f * xx + 1.7f) + 0.06f);
         }
       } else if (kind == FILTER_WINDOW) {  // window.glsl:1-44, FILTER_WINDOW_WIDTH 4
         float acc[3] = {0.0f, 0.0f, 0.0f};
         float weightSum = 0.0f;
         for (int i = 0; i < 4; i++) {
           for (int j = 0; j < 4; j++) {
-            const float wi = ((float)j + 0.5f) * rx / 4.0f, wj = ((float)i + 0.5f) * ry / 4.0f;
-            const float ox = wi / (float)W, oy = wj / (float)H;   // i/512.0, j/512.0 generalised
+            const float wi = fdiv_s(((float)j + 0.5f) * rx, 4.0f), wj = fdiv_s(((float)i + 0.5f) * ry, 4.0f);
+            const float ox = fdiv_s(wi, (float)W), oy = fdiv_s(wj, (float)H);   // i/512.0, j/512.0 generalised
             float tmp[3] = {0.0f, 0.0f, 0.0f};
             int count = 0;
             const float cxs[4] = {tcx + ox, tcx + ox, tcx - ox, tcx - ox};
@@ -1372,7 +1375,7 @@ int oracle_filter(const float* mean, int W, int H, int kind, const float* weight
             acc[0] += tmp[0] * weight; acc[1] += tmp[1] * weight; acc[2] += tmp[2] * weight;
           }
         }
-        o[0] = acc[0] / weightSum; o[1] = acc[1] / weightSum; o[2] = acc[2] / weightSum;
+        o[0] = fdiv_s(acc[0], weightSum); o[1] = fdiv_s(acc[1], weightSum); o[2] = fdiv_s(acc[2], weightSum);
       } else {
         return -2;
       }
@@ -1415,20 +1418,20 @@ int oracle_filter_aov(const float* mean, const float* nrm, const float* pos, int
             float h = 0.0f;
             if (delt % (refm::to_int(stepwidth) + 1) == 0) h = hk[(delt / (refm::to_int(stepwidth) + 1)) % 5];
             if (h == 0.0f) continue;
-            const float u = (tcx - rx / dW) + ((float)j + 0.5f) * rx / dW2;
-            const float v = (tcy - ry / dH) + ((float)i + 0.5f) * ry / dH2;
+            const float u = (tcx - fdiv_s(rx, dW)) + fdiv_s(((float)j + 0.5f) * rx, dW2);
+            const float v = (tcy - fdiv_s(ry, dH)) + fdiv_s(((float)i + 0.5f) * ry, dH2);
             // W() :5-22
             float ctmp[4], ptmp[4], t[4];
             bilinear(mean, W, H, u, v, ctmp); ctmp[3] = 1.0f;
             for (int k = 0; k < 4; k++) t[k] = cval[k] - ctmp[k];
             float dist2 = t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
-            const float c_w = refm::fmin_s(refm::exp_s(-(dist2) / 4.0f), 1.0f);
-            dist2 = refm::fmax_s((t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3]) / (stepwidth * stepwidth), 0.0f);
-            const float n_w = refm::fmin_s(refm::exp_s(-(dist2) / 128.0f), 1.0f);
+            const float c_w = refm::fmin_s(refm::exp_s(fdiv_s(-(dist2), 4.0f)), 1.0f);
+            dist2 = refm::fmax_s(fdiv_s(t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3], stepwidth * stepwidth), 0.0f);
+            const float n_w = refm::fmin_s(refm::exp_s(fdiv_s(-(dist2), 128.0f)), 1.0f);
             bilinear(pos, W, H, u, v, ptmp); ptmp[3] = 1.0f;
             for (int k = 0; k < 4; k++) t[k] = pval[k] - ptmp[k];
             dist2 = t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3];
-            const float p_w = refm::fmin_s(refm::exp_s(-(dist2) / 1.0f), 1.0f);
+            const float p_w = refm::fmin_s(refm::exp_s(fdiv_s(-(dist2), 1.0f)), 1.0f);
             const float weight = c_w * n_w * p_w * h;
             for (int k = 0; k < 4; k++) ctmp[k] *= weight;
             weightSum += weight;
@@ -1436,7 +1439,7 @@ int oracle_filter_aov(const float* mean, const float* nrm, const float* pos, int
           }
         }
       }
-      for (int k = 0; k < 4; k++) o[k] = color[k] / weightSum;
+      for (int k = 0; k < 4; k++) o[k] = fdiv_s(color[k], weightSum);
     }
   }
   return 0;
@@ -1454,10 +1457,11 @@ void oracle_math(int fn, const float* x, const float* y, float* out, int count) 
       case 5: out[i] = refm::pow_s(x[i], y[i]); break;
       case 6: out[i] = refm::atan_s(x[i]); break;
       case 7: out[i] = refm::sqrt_s(x[i]); break;
-      case 8: out[i] = x[i] / y[i]; break;
+      case 8: out[i] = x[i] / y[i]; break;  // IEEE divide
       case 9: out[i] = refm::fmin_s(x[i], y[i]); break;
       case 10: out[i] = refm::fmax_s(x[i], y[i]); break;
-      case 11: out[i] = x[i] / y[i]; break;
+      case 11: out[i] = refm::div_s(x[i], y[i]); break;  // GLSL divide spec
+      case 14: out[i] = refm::rcp_s(x[i]); break;        // its reciprocal
       case 12: out[i] = refm::fmin_s(refm::fmax_s(x[i], 0.0f), 1.0f); break;
       default: out[i] = 0.0f; break;
     }

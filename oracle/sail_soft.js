@@ -13,6 +13,9 @@
 //   or: node oracle/sail_soft.js job.json out.f32   (job: scene rows, masks, W, H, crop, inv, seeds, eye, ...)
 
 const f = Math.fround;
+// GLSL division a / b := a * RN(1/b) (oracle/ref_math.h div_s): f(1 / b) is RN32(1/b) (the f64 quotient of two
+// f32 values never lies within 2^-49 of an f32 rounding midpoint it does not equal) and a * r is exact in f64
+const fdiv = (a, b) => f(a * f(1 / b));
 
 // ---- f32 bit helpers and an exactly rounded f32 fma -------------------------------------------------------
 const _f32 = new Float32Array(1), _u32 = new Uint32Array(_f32.buffer);
@@ -151,10 +154,10 @@ const BLACK = [0, 0, 0], WHITE = [1, 1, 1];
 const vadd = (a, b) => [f(a[0] + b[0]), f(a[1] + b[1]), f(a[2] + b[2])];
 const vsub = (a, b) => [f(a[0] - b[0]), f(a[1] - b[1]), f(a[2] - b[2])];
 const vmul = (a, b) => [f(a[0] * b[0]), f(a[1] * b[1]), f(a[2] * b[2])];
-const vdiv = (a, b) => [f(a[0] / b[0]), f(a[1] / b[1]), f(a[2] / b[2])];
+const vdiv = (a, b) => [fdiv(a[0], b[0]), fdiv(a[1], b[1]), fdiv(a[2], b[2])];
 const vmuls = (a, s) => [f(a[0] * s), f(a[1] * s), f(a[2] * s)];     // a * s
 const smulv = (s, a) => [f(s * a[0]), f(s * a[1]), f(s * a[2])];     // s * a
-const vdivs = (a, s) => [f(a[0] / s), f(a[1] / s), f(a[2] / s)];
+const vdivs = (a, s) => [fdiv(a[0], s), fdiv(a[1], s), fdiv(a[2], s)];
 const vadds = (a, s) => [f(a[0] + s), f(a[1] + s), f(a[2] + s)];
 const vneg = (a) => [-a[0], -a[1], -a[2]];
 const dot = (a, b) => f(f(f(a[0] * b[0]) + f(a[1] * b[1])) + f(a[2] * b[2]));
@@ -187,7 +190,7 @@ function quadratic(A, B, Cc) {  // utility.glsl:37-51 -> null | [t0, t1]
   if (discrim < 0) return null;
   const root = sqrt_(discrim);
   const q = (B < 0) ? f(f(-0.5) * f(B - root)) : f(f(-0.5) * f(B + root));
-  let t0 = f(q / A), t1 = f(Cc / q);
+  let t0 = fdiv(q, A), t1 = fdiv(Cc, q);
   if (t0 > t1) { const tmp = t0; t0 = t1; t1 = tmp; }
   return [t0, t1];
 }
@@ -217,18 +220,18 @@ function fetch(t, cx, cy) {
   if (t.h <= 0) return 0;
   return t.d[texel(cy, t.h) * t.w + texel(cx, t.w)];
 }
-const readFloat = (t, x, y, width) => fetch(t, f(x / width), y);
+const readFloat = (t, x, y, width) => fetch(t, fdiv(x, width), y);
 const readInt = (t, x, y, width) => toint(readFloat(t, x, y, width));
 const readBool = (t, x, y, width) => readInt(t, x, y, width) === 1;
 function readVec3(t, x, y, width) {
-  let px = f(x / width);
-  const step = f(1 / width);
+  let px = fdiv(x, width);
+  const step = fdiv(1, width);
   const a = fetch(t, px, y); px = f(px + step);
   const b = fetch(t, px, y); px = f(px + step);
   return [a, b, fetch(t, px, y)];
 }
-const rowCoord = (i, n) => f(i / (n - 1));
-const matCoord = (v) => f(v / (C.tn - 1));
+const rowCoord = (i, n) => fdiv(i, (n - 1));
+const matCoord = (v) => fdiv(v, (C.tn - 1));
 
 function zeroIns() {
   return { d: 0, hit: BLACK, normal: BLACK, dpdu: BLACK, dpdv: BLACK, into: false, matIndex: 0, sc: BLACK,
@@ -261,8 +264,8 @@ function concentricSampleDisk(u) {
   const uO = f(f(2 * u[0]) - 1), vO = f(f(2 * u[1]) - 1);
   if (uO === 0 && vO === 0) return [0, 0];
   let theta, r;
-  if (Math.abs(uO) > Math.abs(vO)) { r = uO; theta = f(f(vO / uO) * kPiOver4); }
-  else { r = vO; theta = f(kPiOver2 - f(f(uO / vO) * kPiOver4)); }
+  if (Math.abs(uO) > Math.abs(vO)) { r = uO; theta = f(fdiv(vO, uO) * kPiOver4); }
+  else { r = vO; theta = f(kPiOver2 - f(fdiv(uO, vO) * kPiOver4)); }
   return [f(r * cos_(theta)), f(r * sin_(theta))];
 }
 
@@ -275,15 +278,15 @@ function getSurfaceColor(uv, texIndex) {
   switch (cat) {
     case CHECKERBOARD: {
       const size = readFloat(tp, 1, texIndex, kTexLen), lineWidth = readFloat(tp, 2, texIndex, kTexLen);
-      const width = f(f(0.5 * lineWidth) / size);
-      const fx = f(f(uv[0] / size) - floor_(f(uv[0] / size))), fy = f(f(uv[1] / size) - floor_(f(uv[1] / size)));
+      const width = fdiv(f(0.5 * lineWidth), size);
+      const fx = f(fdiv(uv[0], size) - floor_(fdiv(uv[0], size))), fy = f(fdiv(uv[1], size) - floor_(fdiv(uv[1], size)));
       const out = (fx < width || fx > f(1 - width)) || (fy < width || fy > f(1 - width));
       return out ? v3s(0.5) : WHITE;
     }
     case CHECKERBOARD2: {
       const c1 = readVec3(tp, 1, texIndex, kTexLen), c2 = readVec3(tp, 4, texIndex, kTexLen);
       const size = readFloat(tp, 7, texIndex, kTexLen);
-      const qx = floor_(f(uv[0] / size)), qy = floor_(f(uv[1] / size));
+      const qx = floor_(fdiv(uv[0], size)), qy = floor_(fdiv(uv[1], size));
       return (toint(f(qx + qy)) % 2 === 0) ? c1 : c2;
     }
     case BILERP: {
@@ -340,9 +343,9 @@ function dpdBox(normal) {
 function getCubeUV(hit, c) {  // cube.glsl:54-63 (face tests compare hit-min against min: kept)
   const tr = vsub(c.max, c.min);
   hit = vsub(hit, c.min);
-  if (hit[0] < f(c.min[0] + E4) || hit[0] > f(c.max[0] - E4)) return [f(hit[1] / tr[1]), f(hit[2] / tr[2])];
-  if (hit[1] < f(c.min[1] + E4) || hit[1] > f(c.max[1] - E4)) return [f(hit[0] / tr[0]), f(hit[2] / tr[2])];
-  return [f(hit[0] / tr[0]), f(hit[1] / tr[1])];
+  if (hit[0] < f(c.min[0] + E4) || hit[0] > f(c.max[0] - E4)) return [fdiv(hit[1], tr[1]), fdiv(hit[2], tr[2])];
+  if (hit[1] < f(c.min[1] + E4) || hit[1] > f(c.max[1] - E4)) return [fdiv(hit[0], tr[0]), fdiv(hit[2], tr[2])];
+  return [fdiv(hit[0], tr[0]), fdiv(hit[1], tr[1])];
 }
 function intersectCube(ray, c) {
   const r = zeroIns();
@@ -431,16 +434,16 @@ function intersectSphere(ray0, s) {
   if (t >= kMaxDistance) return r;
   const hit = vadd(o, smulv(t, d));
   if (hit[0] === 0 && hit[1] === 0) hit[0] = f(f(1e-5) * s.r);
-  const u = f(phiOf(hit[1], hit[0]) / TWO_PI);
-  const theta = acos_(clamp_(f(hit[2] / s.r), -1, 1));
-  const v = f(theta / kPI);
+  const u = fdiv(phiOf(hit[1], hit[0]), TWO_PI);
+  const theta = acos_(clamp_(fdiv(hit[2], s.r), -1, 1));
+  const v = fdiv(theta, kPI);
   r.d = t;
   r.hit = vadd(o, smulv(t, d));
   {  // computeDpDForSphere :33-43
     const h = r.hit;
-    const th = acos_(clamp_(f(h[2] / s.r), -1, 1));
+    const th = acos_(clamp_(fdiv(h[2], s.r), -1, 1));
     const zRadius = sqrt_(f(f(h[0] * h[0]) + f(h[1] * h[1])));
-    const inv = f(1 / zRadius);
+    const inv = fdiv(1, zRadius);
     const cosPhi = f(h[0] * inv), sinPhi = f(h[1] * inv);
     r.dpdu = dpduRot(h);
     r.dpdv = smulv(kPI, [f(h[2] * cosPhi), f(h[2] * sinPhi), f(-s.r * sin_(th))]);
@@ -457,7 +460,7 @@ function intersectSphere(ray0, s) {
 }
 function sampleSphere(u, s) {
   const p = uniformSampleSphere(u);
-  return [vadd(vmuls(p, s.r), s.c), f(kInvPI / f(s.r * s.r))];
+  return [vadd(vmuls(p, s.r), s.c), fdiv(kInvPI, f(s.r * s.r))];
 }
 
 // ---- rectangle.glsl ---------------------------------------------------------------------------------------
@@ -480,20 +483,20 @@ function intersectRectangle(ray, q) {
   const ss = vdivs(r.dpdu, maxX), ts = cross(r.normal, ss);
   const d = worldToLocal(ray.d, r.normal, ss, ts), o = worldToLocal(vsub(ray.o, q.min), r.normal, ss, ts);
   if (d[2] === 0) return r;
-  const t = f(-o[2] / d[2]);
+  const t = fdiv(-o[2], d[2]);
   if (t < kEps) return r;
   const hit = vadd(o, smulv(t, d));
   if (hit[0] > maxX || hit[1] > maxY || hit[0] < -kEps || hit[1] < -kEps) return r;
   r.d = t;
   r.matIndex = q.matIndex;
-  r.sc = getSurfaceColor([f(hit[0] / maxX), f(hit[1] / maxY)], q.texIndex);
+  r.sc = getSurfaceColor([fdiv(hit[0], maxX), fdiv(hit[1], maxY)], q.texIndex);
   r.emission = q.emission;
   r.hit = vadd(localToWorld(hit, r.normal, ss, ts), q.min);
   return r;
 }
 function sampleRectangle(u, q) {
   const x = rectX(q), y = rectY(q);
-  return [vadd(vadd(q.min, vmuls(x, u[0])), vmuls(y, u[1])), f(1 / f(length(x) * length(y)))];
+  return [vadd(vadd(q.min, vmuls(x, u[0])), vmuls(y, u[1])), fdiv(1, f(length(x) * length(y)))];
 }
 
 // ---- cone.glsl / cylinder.glsl / disk.glsl / hyperboloid.glsl / paraboloid.glsl ----------------------------
@@ -506,9 +509,9 @@ function parseConeCyl(index) {
 const testBoundboxForConeCyl = (ray, c) => testBoundbox(ray, vsub(c.p, [c.r, 0, c.r]), vadd(c.p, [c.r, c.h, c.r]));
 function normalForCone(hit, c) {
   hit = vsub(hit, c.p);
-  const tana = f(c.r / c.h);
+  const tana = fdiv(c.r, c.h);
   const d = sqrt_(f(f(hit[0] * hit[0]) + f(hit[1] * hit[1])));
-  const x1 = f(d / tana), x2 = f(d * tana);
+  const x1 = fdiv(d, tana), x2 = f(d * tana);
   return smulv(sgn(c.rev), normalize(vsub(hit, [0, 0, f(f(c.h - x1) - x2)])));
 }
 const normalForCylinder = (hit, c) => smulv(sgn(c.rev), normalize([f(hit[0] - c.p[0]), f(hit[1] - c.p[1]), 0]));
@@ -542,7 +545,7 @@ function intersectCone(ray0, c) {
   const r = zeroIns();
   r.d = kMaxDistance;
   const d = W2L(ray0.d), o = W2L(vsub(ray0.o, c.p));
-  let k = f(c.r / c.h);
+  let k = fdiv(c.r, c.h);
   k = f(k * k);
   const ozh = f(o[2] - c.h);
   const a = f(f(f(d[0] * d[0]) + f(d[1] * d[1])) - f(f(k * d[2]) * d[2]));
@@ -553,11 +556,11 @@ function intersectCone(ray0, c) {
   const pk = rootPick(q[0], q[1], o, d, -kEps, c.h);
   if (!pk) return r;
   const [t, hit] = pk;
-  const u = f(phiOf(hit[1], hit[0]) / TWO_PI), v = f(hit[2] / c.h);
+  const u = fdiv(phiOf(hit[1], hit[0]), TWO_PI), v = fdiv(hit[2], c.h);
   r.d = t;
-  const vv = f(hit[2] / c.h);
+  const vv = fdiv(hit[2], c.h);
   r.dpdu = dpduRot(hit);
-  r.dpdv = [f(-hit[0] / f(1 - vv)), f(-hit[1] / f(1 - vv)), c.h];
+  r.dpdv = [fdiv(-hit[0], f(1 - vv)), fdiv(-hit[1], f(1 - vv)), c.h];
   return finishLocal(r, hit, [u, v], c.matIndex, c.texIndex, c.emission, c.p);
 }
 function intersectCylinder(ray0, c) {
@@ -572,7 +575,7 @@ function intersectCylinder(ray0, c) {
   const pk = rootPick(q[0], q[1], o, d, -kEps, c.h);
   if (!pk) return r;
   const [t, hit] = pk;
-  const u = f(phiOf(hit[1], hit[0]) / TWO_PI), v = f(hit[2] / c.h);
+  const u = fdiv(phiOf(hit[1], hit[0]), TWO_PI), v = fdiv(hit[2], c.h);
   r.d = t;
   r.dpdu = dpduRot(hit);
   r.dpdv = [0, 0, c.h];
@@ -589,14 +592,14 @@ function intersectDisk(ray0, k) {
   r.d = kMaxDistance;
   const d = W2L(ray0.d), o = W2L(vsub(ray0.o, k.p));
   if (d[2] === 0) return r;
-  const t = f(-o[2] / d[2]);
+  const t = fdiv(-o[2], d[2]);
   if (t <= 0) return r;
   const hit = vadd(o, smulv(t, d));
   const dist2 = f(f(hit[0] * hit[0]) + f(hit[1] * hit[1]));
   if (dist2 > f(k.r * k.r) || dist2 < f(k.innerR * k.innerR)) return r;
   if (t >= kMaxDistance) return r;
-  const u = f(phiOf(hit[1], hit[0]) / TWO_PI);
-  const oneMinusV = f(f(sqrt_(dist2) - k.innerR) / f(k.r - k.innerR));
+  const u = fdiv(phiOf(hit[1], hit[0]), TWO_PI);
+  const oneMinusV = fdiv(f(sqrt_(dist2) - k.innerR), f(k.r - k.innerR));
   const v = f(1 - oneMinusV);
   r.d = t;
   r.dpdu = dpduRot(hit);
@@ -607,7 +610,7 @@ function sampleDisk(u, k) {
   const pd = concentricSampleDisk(u);
   const p = [f(f(pd[0] * k.r) + k.p[0]), k.p[1], f(f(pd[1] * k.r) + k.p[2])];
   const area = f(f(f(2 * kPI) * 0.5) * f(f(k.r * k.r) - f(k.innerR * k.innerR)));
-  return [p, f(1 / area)];
+  return [p, fdiv(1, area)];
 }
 function parseHyperboloid(index) {
   const o = C.objects;
@@ -628,7 +631,7 @@ function hypDpD(hit, p1, p2, phi) {
   return [dpduRot(hit), [f(f(dx * cosPhi) - f(dy * sinPhi)), f(f(dx * sinPhi) + f(dy * cosPhi)), f(p2[2] - p1[2])]];
 }
 function hypPhi(hit, h) {
-  const v = f(f(hit[2] - h.p1[2]) / f(h.p2[2] - h.p1[2]));
+  const v = fdiv(f(hit[2] - h.p1[2]), f(h.p2[2] - h.p1[2]));
   const pr = vadd(smulv(f(1 - v), h.p1), smulv(v, h.p2));
   return [v, phiOf(f(f(pr[0] * hit[1]) - f(hit[0] * pr[1])), f(f(hit[0] * pr[0]) + f(hit[1] * pr[1])))];
 }
@@ -651,7 +654,7 @@ function intersectHyperboloid(ray0, h) {
   if (!pk) return r;
   const [t, hit] = pk;
   const [v, phi] = hypPhi(hit, h);
-  const u = f(phi / TWO_PI);
+  const u = fdiv(phi, TWO_PI);
   r.d = t;
   [r.dpdu, r.dpdv] = hypDpD(hit, h.p1, h.p2, phi);
   return finishLocal(r, hit, [u, v], h.matIndex, h.texIndex, h.emission, h.p);
@@ -669,7 +672,7 @@ function testBoundboxForParaboloid(ray, q) {
 }
 function paraDpD(hit, zMax, zMin) {
   const h2 = f(2 * hit[2]);
-  return [dpduRot(hit), smulv(f(zMax - zMin), [f(hit[0] / h2), f(hit[1] / h2), 1])];
+  return [dpduRot(hit), smulv(f(zMax - zMin), [fdiv(hit[0], h2), fdiv(hit[1], h2), 1])];
 }
 function normalForParaboloid(hit, q) {
   const zMin = fmin_(q.z0, q.z1), zMax = fmax_(q.z0, q.z1);
@@ -681,7 +684,7 @@ function intersectParaboloid(ray0, q) {
   r.d = kMaxDistance;
   const d = W2L(ray0.d), o = W2L(vsub(ray0.o, q.p));
   const zMin = fmin_(q.z0, q.z1), zMax = fmax_(q.z0, q.z1);
-  const k = f(zMax / f(q.r * q.r));
+  const k = fdiv(zMax, f(q.r * q.r));
   const a = f(k * f(f(d[0] * d[0]) + f(d[1] * d[1])));
   const b = f(f(f(2 * k) * f(f(d[0] * o[0]) + f(d[1] * o[1]))) - d[2]);
   const c = f(f(k * f(f(o[0] * o[0]) + f(o[1] * o[1]))) - o[2]);
@@ -690,7 +693,7 @@ function intersectParaboloid(ray0, q) {
   const pk = rootPick(qq[0], qq[1], o, d, zMin, zMax);
   if (!pk) return r;
   const [t, hit] = pk;
-  const u = f(phiOf(hit[1], hit[0]) / TWO_PI), v = f(f(hit[2] - zMin) / f(zMax - zMin));
+  const u = fdiv(phiOf(hit[1], hit[0]), TWO_PI), v = fdiv(f(hit[2] - zMin), f(zMax - zMin));
   r.d = t;
   [r.dpdu, r.dpdv] = paraDpD(hit, zMax, zMin);
   return finishLocal(r, hit, [u, v], q.matIndex, q.texIndex, q.emission, q.p);
@@ -755,21 +758,21 @@ const absCosTheta = (w) => Math.abs(w[2]);
 const cos2Theta = (w) => f(w[2] * w[2]);
 const sin2Theta = (w) => fmax_(0, f(1 - cos2Theta(w)));
 const sinTheta = (w) => sqrt_(sin2Theta(w));
-function tan2Theta(w) { const c2 = cos2Theta(w); return c2 < kEps ? kInf : f(sin2Theta(w) / c2); }
-function cosPhi(w) { const st = sinTheta(w); return equalZero(st) ? 1 : clamp_(f(w[0] / st), -1, 1); }
-function sinPhi(w) { const st = sinTheta(w); return equalZero(st) ? 0 : clamp_(f(w[1] / st), -1, 1); }
+function tan2Theta(w) { const c2 = cos2Theta(w); return c2 < kEps ? kInf : fdiv(sin2Theta(w), c2); }
+function cosPhi(w) { const st = sinTheta(w); return equalZero(st) ? 1 : clamp_(fdiv(w[0], st), -1, 1); }
+function sinPhi(w) { const st = sinTheta(w); return equalZero(st) ? 0 : clamp_(fdiv(w[1], st), -1, 1); }
 const cos2Phi = (w) => f(cosPhi(w) * cosPhi(w));
 const sin2Phi = (w) => f(sinPhi(w) * sinPhi(w));
 const sameHemisphere = (w, wp) => f(w[2] * wp[2]) > kEps;
 function frDielectric(cosThetaI, etaI, etaT) {
   cosThetaI = clamp_(cosThetaI, -1, 1);
   const sinThetaI = sqrt_(fmax_(0, f(1 - f(cosThetaI * cosThetaI))));
-  const sinThetaT = f(f(etaI / etaT) * sinThetaI);
+  const sinThetaT = f(fdiv(etaI, etaT) * sinThetaI);
   if (sinThetaT >= 1) return 1;
   const cosThetaT = sqrt_(fmax_(0, f(1 - f(sinThetaT * sinThetaT))));
   const TI = f(etaT * cosThetaI), IT = f(etaI * cosThetaT), II = f(etaI * cosThetaI), TT = f(etaT * cosThetaT);
-  const Rparl = f(f(TI - IT) / f(TI + IT)), Rperp = f(f(II - TT) / f(II + TT));
-  return f(f(f(Rparl * Rparl) + f(Rperp * Rperp)) / 2);
+  const Rparl = fdiv(f(TI - IT), f(TI + IT)), Rperp = fdiv(f(II - TT), f(II + TT));
+  return fdiv(f(f(Rparl * Rparl) + f(Rperp * Rperp)), 2);
 }
 function frConductor(cosThetaI, etaI, etaT, k) {
   cosThetaI = clamp_(cosThetaI, -1, 1);
@@ -797,16 +800,16 @@ function frEvaluate(fr, cosThetaI) {
 function trSampleWh(u, ax, ay, wo) {
   let cosT = 0, phi = f(TWO_PI * u[0]);
   if (ax === ay) {
-    const tanTheta2 = f(f(f(ax * ax) * u[0]) / f(1 - u[0]));
-    cosT = f(1 / sqrt_(f(1 + tanTheta2)));
+    const tanTheta2 = fdiv(f(f(ax * ax) * u[0]), f(1 - u[0]));
+    cosT = fdiv(1, sqrt_(f(1 + tanTheta2)));
   } else {
-    phi = atan_(f(f(ay / ax) * tan_(f(kPiOver2 + f(TWO_PI * u[0])))));
+    phi = atan_(f(fdiv(ay, ax) * tan_(f(kPiOver2 + f(TWO_PI * u[0])))));
     if (u[0] > 0.5) phi = f(phi + kPI);
     const [sP, cP] = sincos(phi);
     const ax2 = f(ax * ax), ay2 = f(ay * ay);
-    const alpha2 = f(1 / f(f(f(cP * cP) / ax2) + f(f(sP * sP) / ay2)));
-    const tanTheta2 = f(f(alpha2 * u[0]) / f(1 - u[0]));
-    cosT = f(1 / sqrt_(f(1 + tanTheta2)));
+    const alpha2 = fdiv(1, f(fdiv(f(cP * cP), ax2) + fdiv(f(sP * sP), ay2)));
+    const tanTheta2 = fdiv(f(alpha2 * u[0]), f(1 - u[0]));
+    cosT = fdiv(1, sqrt_(f(1 + tanTheta2)));
   }
   const sinT = sqrt_(fmax_(0, f(1 - f(cosT * cosT))));
   const [sp, cp] = sincos(phi);
@@ -818,9 +821,9 @@ function trD(ax, ay, wh) {
   const t2 = tan2Theta(wh);
   if (t2 >= kInf) return f(0.001);
   const cos4 = f(cos2Theta(wh) * cos2Theta(wh));
-  const e = f(f(f(cos2Phi(wh) / f(ax * ax)) + f(sin2Phi(wh) / f(ay * ay))) * t2);
+  const e = f(f(fdiv(cos2Phi(wh), f(ax * ax)) + fdiv(sin2Phi(wh), f(ay * ay))) * t2);
   const ope = f(1 + e);
-  return f(1 / f(f(f(f(f(kPI * ax) * ay) * cos4) * ope) * ope));
+  return fdiv(1, f(f(f(f(f(kPI * ax) * ay) * cos4) * ope) * ope));
 }
 const trPdf = (ax, ay, wh) => f(trD(ax, ay, wh) * absCosTheta(wh));
 function orenNayarF(R, A, B, wo, wi) {
@@ -831,8 +834,8 @@ function orenNayarF(R, A, B, wo, wi) {
     maxCos = fmax_(0, f(f(cosPhiI * cosPhiO) + f(sinPhiI * sinPhiO)));
   }
   let sinAlpha, tanBeta;
-  if (absCosTheta(wi) > absCosTheta(wo)) { sinAlpha = sinThetaO; tanBeta = f(sinThetaI / absCosTheta(wi)); }
-  else { sinAlpha = sinThetaI; tanBeta = f(sinThetaO / absCosTheta(wo)); }
+  if (absCosTheta(wi) > absCosTheta(wo)) { sinAlpha = sinThetaO; tanBeta = fdiv(sinThetaI, absCosTheta(wi)); }
+  else { sinAlpha = sinThetaI; tanBeta = fdiv(sinThetaO, absCosTheta(wo)); }
   return vmuls(vmuls(R, kInvPI), f(A + f(f(f(B * maxCos) * sinAlpha) * tanBeta)));
 }
 const TINY = vmuls(BLACK, f(0.001));
@@ -850,34 +853,34 @@ function microRSample(mr, u, wo, out) {
   const wh = trSampleWh(u, mr.ax, mr.ay, wo);
   out.wi = reflect_(vneg(wo), wh);
   if (!sameHemisphere(wo, out.wi)) return TINY;
-  out.pdf = f(trPdf(mr.ax, mr.ay, wh) / f(4 * dot(wo, wh)));
+  out.pdf = fdiv(trPdf(mr.ax, mr.ay, wh), f(4 * dot(wo, wh)));
   return microRF(mr, wo, out.wi);
 }
 function microTF(mt, wo, wi) {
   if (sameHemisphere(wo, wi)) return TINY;
   const cosThetaO = wo[2], cosThetaI = wi[2];
   if (equalZero(cosThetaI) || equalZero(cosThetaO)) return TINY;
-  const eta = mt.into ? f(mt.etaB / mt.etaA) : f(mt.etaA / mt.etaB);
+  const eta = mt.into ? fdiv(mt.etaB, mt.etaA) : fdiv(mt.etaA, mt.etaB);
   let wh = normalize(vadd(wo, vmuls(wi, eta)));
   if (wh[2] < -kEps) wh = vneg(wh);
   const Fd = frDielectric(dot(wo, wh), mt.etaA, mt.etaB);
   const sqrtDenom = f(dot(wo, wh) + f(eta * dot(wi, wh)));
   const num = f(f(f(f(f(eta * eta) * trD(mt.ax, mt.ay, wh)) * Math.abs(dot(wi, wh))) * Math.abs(dot(wo, wh))));
   const den = f(f(f(cosThetaI * cosThetaO) * sqrtDenom) * sqrtDenom);
-  return vmuls(smulv(f(1 - Fd), mt.T), Math.abs(f(num / den)));
+  return vmuls(smulv(f(1 - Fd), mt.T), Math.abs(fdiv(num, den)));
 }
 function microTPdf(mt, wo, wi) {
   if (sameHemisphere(wo, wi)) return f(0.001);
-  const eta = mt.into ? f(mt.etaB / mt.etaA) : f(mt.etaA / mt.etaB);
+  const eta = mt.into ? fdiv(mt.etaB, mt.etaA) : fdiv(mt.etaA, mt.etaB);
   const wh = normalize(vadd(wo, vmuls(wi, eta)));
   const sqrtDenom = f(dot(wo, wh) + f(eta * dot(wi, wh)));
-  const dwh = Math.abs(f(f(f(eta * eta) * dot(wi, wh)) / f(sqrtDenom * sqrtDenom)));
+  const dwh = Math.abs(fdiv(f(f(eta * eta) * dot(wi, wh)), f(sqrtDenom * sqrtDenom)));
   return f(trPdf(mt.ax, mt.ay, wh) * dwh);
 }
 function microTSample(mt, u, wo, out) {
   if (equalZero(wo[2])) return TINY;
   const wh = trSampleWh(u, mt.ax, mt.ay, wo);
-  const eta = mt.into ? f(mt.etaA / mt.etaB) : f(mt.etaB / mt.etaA);
+  const eta = mt.into ? fdiv(mt.etaA, mt.etaB) : fdiv(mt.etaB, mt.etaA);
   out.wi = refract_(vneg(wo), wh, eta);
   out.pdf = microTPdf(mt, wo, out.wi);
   return microTF(mt, wo, out.wi);
@@ -929,7 +932,7 @@ function glass(u, mi, sc, wo, into, out) {
       fs = vdivs(R, absCosTheta(out.wi));
     } else {
       const etaI = into ? 1 : eta, etaT = into ? eta : 1;
-      out.wi = refract_(vneg(wo), [0, 0, 1], f(etaI / etaT));
+      out.wi = refract_(vneg(wo), [0, 0, 1], fdiv(etaI, etaT));
       out.pdf = 1;
       fs = vdivs(vmuls(T, f(1 - Fd)), absCosTheta(out.wi));
     }
@@ -992,7 +995,7 @@ function lightSample(ins) {
     let fall;
     if (cT < ctw) fall = 0;
     else if (cT >= cfs) fall = 1;
-    else { const delta = f(f(cT - ctw) / f(cfs - ctw)); const d2 = f(delta * delta); fall = f(d2 * d2); }
+    else { const delta = fdiv(f(cT - ctw), f(cfs - ctw)); const d2 = f(delta * delta); fall = f(d2 * d2); }
     return vdivs(vmuls(vmuls(em, fall), fmax_(0, dot(normalize(toLight), ins.normal))), f(d * d));
   }
   return BLACK;
@@ -1034,7 +1037,7 @@ function cornerDirs(M, eye) {  // M: 16 f32, column-major
   for (let c = 0; c < 4; c++) {
     const q = [];
     for (let r = 0; r < 4; r++) q.push(f(f(f(f(M[r] * cx[c]) + f(M[4 + r] * cy[c])) + f(M[8 + r] * 0)) + f(M[12 + r] * 1)));
-    const w = [f(q[0] / q[3]), f(q[1] / q[3]), f(q[2] / q[3])];
+    const w = [fdiv(q[0], q[3]), fdiv(q[1], q[3]), fdiv(q[2], q[3])];
     out.push(normalize(vsub(w, eye)));
   }
   return out;
@@ -1103,9 +1106,10 @@ function mathFn(fn, x, y) {
     case 8: return f(x / y);
     case 9: return fmin_(x, y);
     case 10: return fmax_(x, y);
-    case 11: return f(x / y);
+    case 11: return fdiv(x, y);  // GLSL divide spec
     case 12: return clamp_(x, 0, 1);
     case 13: return fma32(x, y, f(0.25));  // the exact f32 fma itself
+    case 14: return f(1 / x);
     default: return NaN;
   }
 }

@@ -54,6 +54,10 @@ struct Rccl {
 Rccl g_rccl;
 constexpr int kNcclFloat32 = 7, kNcclSum = 0;
 
+// GLSL division on the host, for the shader expressions evaluated here once per scene or per sample: the math
+// spec's a * RN(1/b) (sail_math.h fdiv, oracle/ref_math.h div_s); host f32 arithmetic is IEEE (no contraction)
+float gdiv(float a, float b) { return a * (1.0f / b); }
+
 // ---- the reference's texture addressing (texhelper.glsl, NEAREST + CLAMP_TO_EDGE) ----------------------
 int texel(float c, int size) {
   if (c != c) return 0;  // NaN row coordinate (n = 1 / ln = 1: 0/0) addresses texel 0
@@ -74,11 +78,11 @@ struct TexView {
     if (h <= 0) return 0.0f;
     return d[texel(cy, h) * w + texel(cx, w)];
   }
-  float readFloat(float x, float y, float width) const { return at(x / width, y); }
+  float readFloat(float x, float y, float width) const { return at(gdiv(x, width), y); }
   void readVec3(float x, float y, float width, float* out) const {
-    float px = x / width;
-    out[0] = at(px, y); px += 1.0f / width;
-    out[1] = at(px, y); px += 1.0f / width;
+    float px = gdiv(x, width);
+    out[0] = at(px, y); px += gdiv(1.0f, width);
+    out[1] = at(px, y); px += gdiv(1.0f, width);
     out[2] = at(px, y);
   }
 };
@@ -206,9 +210,9 @@ void cornerDirs(const float* M, const float* eye, float out[4][3]) {
   for (int c = 0; c < 4; c++) {
     float q[4];
     for (int r = 0; r < 4; r++) q[r] = M[0 * 4 + r] * cx[c] + M[1 * 4 + r] * cy[c] + M[2 * 4 + r] * 0.0f + M[3 * 4 + r] * 1.0f;
-    const float w[3] = {q[0] / q[3] - eye[0], q[1] / q[3] - eye[1], q[2] / q[3] - eye[2]};
+    const float w[3] = {gdiv(q[0], q[3]) - eye[0], gdiv(q[1], q[3]) - eye[1], gdiv(q[2], q[3]) - eye[2]};
     const float len = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-    out[c][0] = w[0] / len; out[c][1] = w[1] / len; out[c][2] = w[2] / len;
+    out[c][0] = gdiv(w[0], len); out[c][1] = gdiv(w[1], len); out[c][2] = gdiv(w[2], len);
   }
 }
 
@@ -239,7 +243,7 @@ int resetAccum(sail_ctx* c) {
 struct F3 { float x, y, z; };
 F3 f3cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 float f3dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-F3 f3div(F3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+F3 f3div(F3 a, float s) { return {gdiv(a.x, s), gdiv(a.y, s), gdiv(a.z, s)}; }
 void rectFrameHost(SailPrim& p) {
   const F3 dpdu{p.a[3] - p.a[0], 0.0f, 0.0f}, dpdv{0.0f, p.a[4] - p.a[1], p.a[5] - p.a[2]};
   const F3 cr = f3cross(dpdu, dpdv);
@@ -248,7 +252,7 @@ void rectFrameHost(SailPrim& p) {
   const F3 ss = f3div(dpdu, maxX);
   const F3 ts = f3cross(normal, ss);
   const float f[12] = {normal.x, normal.y, normal.z, ss.x, ss.y, ss.z, ts.x, ts.y, ts.z, maxX, maxY,
-                       1.0f / (maxX * maxY)};
+                       gdiv(1.0f, maxX * maxY)};
   memcpy(&p.a[6], f, sizeof f);
 }
 
@@ -260,12 +264,12 @@ float hwmax(float a, float b) { if (a != a) return b; if (b != b) return a; if (
 //   hyperboloid (hyperboloid.glsl:13-24)  a[11] = max(r1, r2), a[12] = min(p1.z, p2.z), a[13] = max(p1.z, p2.z)
 //   paraboloid (paraboloid.glsl:60)   a[6] = zMax / (rad * rad)
 void quadricHost(SailPrim& p) {
-  if (p.type == SAIL_CONE) { float k = p.a[4] / p.a[3]; p.a[5] = k * k; }
+  if (p.type == SAIL_CONE) { float k = gdiv(p.a[4], p.a[3]); p.a[5] = k * k; }
   if (p.type == SAIL_HYPERBOLOID) {
     const float r1 = sqrtf(p.a[3] * p.a[3] + p.a[4] * p.a[4]), r2 = sqrtf(p.a[6] * p.a[6] + p.a[7] * p.a[7]);
     p.a[11] = hwmax(r1, r2); p.a[12] = hwmin(p.a[5], p.a[8]); p.a[13] = hwmax(p.a[5], p.a[8]);
   }
-  if (p.type == SAIL_PARABOLOID) p.a[6] = hwmax(p.a[3], p.a[4]) / (p.a[5] * p.a[5]);
+  if (p.type == SAIL_PARABOLOID) p.a[6] = gdiv(hwmax(p.a[3], p.a[4]), p.a[5] * p.a[5]);
 }
 
 // Conservative world-space bounds of what each primitive's intersection can return, padded, in a[18..23]
@@ -335,9 +339,9 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
   const float L = 17.0f;
   out.assign((size_t)n, SailPrim{});
   *anyHitOk = 1;
-  auto row = [&](float v) { return texel(v / (float)(tn - 1), tn); };
+  auto row = [&](float v) { return texel(gdiv(v, (float)(tn - 1)), tn); };
   for (int i = 0; i < n; i++) {
-    const float rc = (float)i / (float)(n - 1);
+    const float rc = gdiv((float)i, (float)(n - 1));
     SailPrim& p = out[i];
     memset(&p, 0, sizeof p);
     const int cat = to_int(o.at(0.0f, rc));
@@ -601,9 +605,9 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
   for (int r = 0; r < ln; r++) {
-    const float rc = (ln == 1) ? NAN : (float)r / (float)(ln - 1);
+    const float rc = (ln == 1) ? NAN : gdiv((float)r, (float)(ln - 1));
     const int gi = to_int(lv.readFloat(1.0f, rc, 17.0f));
-    lrow[r] = (n > 0) ? texel((float)gi / (float)(n - 1), n) : 0;
+    lrow[r] = (n > 0) ? texel(gdiv((float)gi, (float)(n - 1)), n) : 0;
   }
   void* old[] = {c->prims, c->tp, c->lt, c->lightObjRow};
   for (void* b : old) if (b) HIPCHK(c, hipFree(b));

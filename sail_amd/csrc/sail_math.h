@@ -160,6 +160,18 @@ SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 SM_D float clamp_(float x, float lo, float hi) { return fmin_(fmax_(x, lo), hi); }
 SM_D float fract_(float x) { return x - floorf(x); }
 SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }
+// GLSL division a / b := a * RN(1/b) (the reciprocal-multiply form shader compilers emit, with the reciprocal
+// correctly rounded; oracle/ref_math.h div_s). RN(1/b) = one Newton step from the hardware reciprocal, equal to
+// the IEEE 1.0f / b for every f32 b with 2^-126 <= |b| <= 2^126 (all 2^32 inputs checked on an MI355X:
+// tools/rcp_probe.hip); zero, inf, NaN, subnormal and huge divisors take the IEEE divide. Literal divisors fold.
+SM_D float rcp_rn(float b) {
+  if (__builtin_constant_p(b)) return 1.0f / b;
+  const float ab = __builtin_fabsf(b);
+  if (__builtin_expect(!(ab >= 0x1p-126f && ab <= 0x1p126f), 0)) return 1.0f / b;
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  return fma_(fma_(-b, y0, 1.0f), y0, y0);
+}
+SM_D float fdiv(float a, float b) { return a * rcp_rn(b); }
 SM_D int to_int(float x) {
   if (x != x) return 0;
   if (x >= 2147483647.0f) return 2147483647;

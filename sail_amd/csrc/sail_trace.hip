@@ -27,12 +27,6 @@
 
 using namespace sm;
 
-#ifndef SAIL_FAST_RCP
-#define SAIL_FAST_RCP 1
-#endif
-#ifndef SAIL_XDIV_NORMALIZE
-#define SAIL_XDIV_NORMALIZE 0
-#endif
 #ifndef SAIL_SWEEP_HL
 #define SAIL_SWEEP_HL 1
 #endif
@@ -59,10 +53,11 @@ D V2 v2(float x, float y) { V2 r; r.x = x; r.y = y; return r; }
 D V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 D V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 D V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-D V3 operator/(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }
+// GLSL division (sail_math.h fdiv: a * RN(1/b)); a vector over a scalar shares one reciprocal
+D V3 operator/(V3 a, V3 b) { return v3(fdiv(a.x, b.x), fdiv(a.y, b.y), fdiv(a.z, b.z)); }
 D V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 D V3 operator*(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
-D V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+D V3 operator/(V3 a, float s) { const float r = rcp_rn(s); return v3(a.x * r, a.y * r, a.z * r); }
 D V3 operator+(V3 a, float s) { return v3(a.x + s, a.y + s, a.z + s); }
 D V3 operator-(V3 a, float s) { return v3(a.x - s, a.y - s, a.z - s); }
 D V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
@@ -70,17 +65,7 @@ D V2 operator*(float s, V2 a) { return v2(s * a.x, s * a.y); }
 D float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 D V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 D float length(V3 v) { return sqrtf_(dot(v, v)); }
-D float xdiv(float a, float b, double rb);
-D double rcp_exact(float b);
-#if SAIL_XDIV_NORMALIZE
-D V3 normalize(V3 v) {
-  const float len = length(v);
-  const double rl = rcp_exact(len);
-  return v3(xdiv(v.x, len, rl), xdiv(v.y, len, rl), xdiv(v.z, len, rl));
-}
-#else
 D V3 normalize(V3 v) { return v / length(v); }
-#endif
 D V3 vmin(V3 a, V3 b) { return v3(fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)); }
 D V3 vmax(V3 a, V3 b) { return v3(fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)); }
 D V3 vclamp01(V3 x) { return vmin(vmax(x, v3s(0.0f)), v3s(1.0f)); }
@@ -110,42 +95,19 @@ D bool quadratic(float A, float B, float C, float& t0, float& t1) {  // utility.
   float q;
   if (B < 0.0f) q = -0.5f * (B - rootDiscrim);
   else q = -0.5f * (B + rootDiscrim);
-  t0 = q / A;
-  t1 = C / q;
+  t0 = fdiv(q, A);
+  t1 = fdiv(C, q);
   if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
   return true;
 }
 
-// A ray carries the f64 reciprocals of its direction: every slab test divides by the same three
-// components, and a/b == RN_f32(RN_f64(a * RN_f64(1/b))) for all f32 a, b except results that are
-// nonzero subnormals (the f64 product is within 2^-52 of a/b, while a/b of two floats is never within
-// 2^-49 of an f32 rounding midpoint it does not equal) -- those take the IEEE f32 divide (xdiv).
-struct Ray { V3 o, d; double rx, ry, rz; };
-// f64 reciprocal of an f32 with relative error <= ~2^-52 (what xdiv needs): an f32 hardware reciprocal
-// refined by two f64 Newton steps; zero/inf/NaN/extreme magnitudes take the IEEE f64 divide.
-D double rcp_exact(float b) {
-#if SAIL_FAST_RCP
-  const float ab = fabsf(b);
-  if (!(ab >= 0x1p-120f && ab <= 0x1p120f)) return 1.0 / (double)b;
-  const double bd = (double)b;
-  double r = (double)__builtin_amdgcn_rcpf(b);
-  double e = __builtin_fma(-bd, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-bd, r, 1.0);
-  return __builtin_fma(r, e, r);
-#else
-  return 1.0 / (double)b;
-#endif
-}
+// A ray carries the reciprocals of its direction: every slab test divides by the same three components, and
+// under the GLSL division spec a / d.x is a * RN(1/d.x), so a slab is six subtractions and six multiplies.
+struct Ray { V3 o, d; float rx, ry, rz; };
 D Ray mkRay(V3 o, V3 d) {
   Ray r; r.o = o; r.d = d;
-  r.rx = rcp_exact(d.x); r.ry = rcp_exact(d.y); r.rz = rcp_exact(d.z);
+  r.rx = rcp_rn(d.x); r.ry = rcp_rn(d.y); r.rz = rcp_rn(d.z);
   return r;
-}
-D float xdiv(float a, float b, double rb) {
-  const float q = (float)((double)a * rb);
-  if (__builtin_expect(fabsf(q) < 0x1p-126f && q != 0.0f, 0)) return a / b;
-  return q;
 }
 // ---- optional phase timing (tools: -DSAIL_PHASE_TIMING=1 variant builds only): per-wave s_memtime deltas
 #ifndef SAIL_PHASE_TIMING
@@ -221,8 +183,8 @@ D V2 concentricSampleDisk(V2 u) {
   const float uOffset = 2.0f * u.x - 1.0f, vOffset = 2.0f * u.y - 1.0f;
   if (uOffset == 0.0f && vOffset == 0.0f) return v2(0.0f, 0.0f);
   float theta, r;
-  if (fabsf(uOffset) > fabsf(vOffset)) { r = uOffset; theta = (vOffset / uOffset) * kPiOver4; }
-  else { r = vOffset; theta = kPiOver2 - (uOffset / vOffset) * kPiOver4; }
+  if (fabsf(uOffset) > fabsf(vOffset)) { r = uOffset; theta = fdiv(vOffset, uOffset) * kPiOver4; }
+  else { r = vOffset; theta = kPiOver2 - fdiv(uOffset, vOffset) * kPiOver4; }
   float s, co; sincosf_(theta, s, co);
   return r * v2(co, s);
 }
@@ -237,14 +199,14 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
   switch (cat) {
     case SAIL_TEX_CHECKERBOARD: if (!HAS(c.kTex, SAIL_TEX_CHECKERBOARD)) break; {
       const float size = TP(c, texRow, 1), lineWidth = TP(c, texRow, 2);
-      const float width = 0.5f * lineWidth / size;
-      const float fx = uv.x / size - floorf(uv.x / size), fy = uv.y / size - floorf(uv.y / size);
+      const float width = fdiv(0.5f * lineWidth, size);
+      const float fx = fdiv(uv.x, size) - floorf(fdiv(uv.x, size)), fy = fdiv(uv.y, size) - floorf(fdiv(uv.y, size));
       const bool in_outline = (fx < width || fx > 1.0f - width) || (fy < width || fy > 1.0f - width);
       return in_outline ? v3s(0.5f) : v3s(1.0f);
     }
     case SAIL_TEX_CHECKERBOARD2: if (!HAS(c.kTex, SAIL_TEX_CHECKERBOARD2)) break; {
       const float size = TP(c, texRow, 7);
-      const float qx = floorf(uv.x / size), qy = floorf(uv.y / size);
+      const float qx = floorf(fdiv(uv.x, size)), qy = floorf(fdiv(uv.y, size));
       return (to_int(qx + qy) % 2 == 0) ? TP3(c, texRow, 1) : TP3(c, texRow, 4);
     }
     case SAIL_TEX_BILERP: if (!HAS(c.kTex, SAIL_TEX_BILERP)) break; {
@@ -267,8 +229,8 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
 struct Slab { float tNear, tFar; };
 D Slab slab(V3 bmin, V3 bmax, const Ray& r) {
   const V3 a0 = bmin - r.o, a1 = bmax - r.o;
-  const V3 tMin = v3(xdiv(a0.x, r.d.x, r.rx), xdiv(a0.y, r.d.y, r.ry), xdiv(a0.z, r.d.z, r.rz));
-  const V3 tMax = v3(xdiv(a1.x, r.d.x, r.rx), xdiv(a1.y, r.d.y, r.ry), xdiv(a1.z, r.d.z, r.rz));
+  const V3 tMin = v3(a0.x * r.rx, a0.y * r.ry, a0.z * r.rz);  // (bmin - o) / d
+  const V3 tMax = v3(a1.x * r.rx, a1.y * r.ry, a1.z * r.rz);
   const V3 t1 = vmin(tMin, tMax), t2 = vmax(tMin, tMax);
   Slab s;
   s.tNear = fmax_(fmax_(t1.x, t1.y), t1.z);
@@ -326,9 +288,9 @@ D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
   if (needsUV(c, p.texRow)) {
     const V3 mn = P3(p, 0), mx = P3(p, 3);
     const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
-    if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(hh.y / tr.y, hh.z / tr.z);
-    else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(hh.x / tr.x, hh.z / tr.z);
-    else uv = v2(hh.x / tr.x, hh.y / tr.y);
+    if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(fdiv(hh.y, tr.y), fdiv(hh.z, tr.z));
+    else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(fdiv(hh.x, tr.x), fdiv(hh.z, tr.z));
+    else uv = v2(fdiv(hh.x, tr.x), fdiv(hh.y, tr.y));
   }
   h.sc = getSurfaceColor(c, uv, p.texRow);
 }
@@ -381,16 +343,16 @@ D V3 dpduRot(V3 hit) { return v3(-2.0f * kPI * hit.y, 2.0f * kPI * hit.x, 0.0f);
 D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const float rad = p.a[3];
   // theta of the UV and of computeDpDForSphere (:33-43) are the same value: the pole guard touches x only
-  const float theta = acosf_(clamp_(hl.z / rad, -1.0f, 1.0f));
+  const float theta = acosf_(clamp_(fdiv(hl.z, rad), -1.0f, 1.0f));
   V2 uv = v2(0.0f, 0.0f);
   if (needsUV(c, p.texRow)) {
     V3 hit = hl;
     if (hit.x == 0.0f && hit.y == 0.0f) hit.x = 1e-5f * rad;
-    uv = v2(phiOf(hit.y, hit.x) / (2.0f * kPI), theta / kPI);
+    uv = v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(theta, kPI));
   }
   const float th2 = theta;
   const float zRadius = sqrtf_(hl.x * hl.x + hl.y * hl.y);
-  const float invZRadius = 1.0f / zRadius;
+  const float invZRadius = rcp_rn(zRadius);
   const float cosPhi = hl.x * invZRadius, sinPhi = hl.y * invZRadius;
   const V3 dpdu = dpduRot(hl);
   const V3 dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(th2));
@@ -418,7 +380,7 @@ D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
   const V3 d = worldToLocal(r.d, f.normal, f.ss, f.ts);
   const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
   if (d.z == 0.0f) return kMaxDistance;
-  const float t = -o.z / d.z;
+  const float t = fdiv(-o.z, d.z);
   if (t < kEps) return kMaxDistance;
   const V3 hit = o + t * d;
   if (hit.x > f.maxX || hit.y > f.maxY || hit.x < -kEps || hit.y < -kEps) return kMaxDistance;
@@ -428,7 +390,7 @@ D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
 D void rectHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const RectFrame f = rectFrame(p);
   h.dpdu = f.dpdu; h.dpdv = f.dpdv; h.normal = f.normal;
-  h.sc = getSurfaceColor(c, needsUV(c, p.texRow) ? v2(hl.x / f.maxX, hl.y / f.maxY) : v2(0.0f, 0.0f), p.texRow);
+  h.sc = getSurfaceColor(c, needsUV(c, p.texRow) ? v2(fdiv(hl.x, f.maxX), fdiv(hl.y, f.maxY)) : v2(0.0f, 0.0f), p.texRow);
   h.hit = localToWorld(hl, f.normal, f.ss, f.ts) + P3(p, 0);
 }
 
@@ -543,7 +505,7 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
   const float rad = p.a[3], ri = p.a[4];
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   if (d.z == 0.0f) return kMaxDistance;
-  const float t = -o.z / d.z;
+  const float t = fdiv(-o.z, d.z);
   if (t <= 0.0f) return kMaxDistance;
   const V3 hit = o + t * d;
   const float dist2 = hit.x * hit.x + hit.y * hit.y;
@@ -563,14 +525,14 @@ D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dp
 }
 D void coneHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
-  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
-  const float vv = hit.z / hh;
-  const V3 dpdv = v3(-hit.x / (1.0f - vv), -hit.y / (1.0f - vv), hh);
+  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
+  const float vv = fdiv(hit.z, hh);
+  const V3 dpdv = v3(fdiv(-hit.x, 1.0f - vv), fdiv(-hit.y, 1.0f - vv), hh);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
 D void cylinderHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
-  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), hit.z / hh) : v2(0.0f, 0.0f);
+  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
   finishLocal(c, p, hit, uv, dpduRot(hit), v3(0.0f, 0.0f, hh), h);
 }
 D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperboloid.glsl:41-46
@@ -580,21 +542,21 @@ D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperbo
 }
 D void hypHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const V3 p1 = P3(p, 3), p2 = P3(p, 6);
-  const float v = (hit.z - p1.z) / (p2.z - p1.z);
+  const float v = fdiv(hit.z - p1.z, p2.z - p1.z);
   const V3 pr = (1.0f - v) * p1 + v * p2;
   const float phi = phiOf(pr.x * hit.y - hit.x * pr.y, hit.x * pr.x + hit.y * pr.y);
-  const float u = phi / (2.0f * kPI);
+  const float u = fdiv(phi, 2.0f * kPI);
   V3 dpdu, dpdv;
   hypDpD(hit, p1, p2, phi, dpdu, dpdv);
   finishLocal(c, p, hit, v2(u, v), dpdu, dpdv, h);
 }
 D void paraDpD(V3 hit, float zMax, float zMin, V3& dpdu, V3& dpdv) {  // paraboloid.glsl:35-40
   dpdu = dpduRot(hit);
-  dpdv = (zMax - zMin) * v3(hit.x / (2.0f * hit.z), hit.y / (2.0f * hit.z), 1.0f);
+  dpdv = (zMax - zMin) * v3(fdiv(hit.x, 2.0f * hit.z), fdiv(hit.y, 2.0f * hit.z), 1.0f);
 }
 D void paraHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
-  const V2 uv = needsUV(c, p.texRow) ? v2(phiOf(hit.y, hit.x) / (2.0f * kPI), (hit.z - zMin) / (zMax - zMin)) : v2(0.0f, 0.0f);
+  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z - zMin, zMax - zMin)) : v2(0.0f, 0.0f);
   V3 dpdu, dpdv;
   paraDpD(hit, zMax, zMin, dpdu, dpdv);
   finishLocal(c, p, hit, uv, dpdu, dpdv, h);
@@ -605,8 +567,8 @@ D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   V2 uv = v2(0.0f, 0.0f);
   if (needsUV(c, p.texRow)) {
     const float rHit = sqrtf_(dist2);
-    const float oneMinusV = ((rHit - ri) / (rad - ri));
-    uv = v2(phiOf(hit.y, hit.x) / (2.0f * kPI), 1.0f - oneMinusV);
+    const float oneMinusV = fdiv(rHit - ri, rad - ri);
+    uv = v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), 1.0f - oneMinusV);
   }
   const V3 dpdv = v3(hit.x, hit.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
@@ -633,7 +595,7 @@ D float primT(const Ctx& c, const SailPrim& p, const Ray& r, V3* hl) {
 // primBoundsHost). It rejects only rays that miss the padded box or enter it beyond the closest distance so
 // far (with margin); such a primitive's exact test could only return a miss or a larger distance.
 D bool padHit(const SailPrim& p, const Ray& r, float best) {
-  const float ix = (float)r.rx, iy = (float)r.ry, iz = (float)r.rz;
+  const float ix = r.rx, iy = r.ry, iz = r.rz;
   const float x0 = (p.a[18] - r.o.x) * ix, x1 = (p.a[21] - r.o.x) * ix;
   const float y0 = (p.a[19] - r.o.y) * iy, y1 = (p.a[22] - r.o.y) * iy;
   const float z0 = (p.a[20] - r.o.z) * iz, z1 = (p.a[23] - r.o.z) * iz;
@@ -828,7 +790,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
       const V3 q = uniformSampleSphere(u);
       const float rad = p.a[3];
-      pdf = kInvPI / (rad * rad);
+      pdf = fdiv(kInvPI, rad * rad);
       const V3 res = q * rad + P3(p, 0);
       normal = s * (res - P3(p, 0)) / rad;
       return res;
@@ -847,7 +809,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
       const float rad = p.a[3], ri = p.a[4];
       const V3 res = v3(pd.x * rad + pp.x, pp.y, pd.y * rad + pp.z);
       const float area = 2.0f * kPI * 0.5f * (rad * rad - ri * ri);
-      pdf = 1.0f / area;
+      pdf = rcp_rn(area);
       normal = s * v3(0.0f, 1.0f, 0.0f);
       return res;
     }
@@ -856,9 +818,9 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
     case SAIL_CONE: {  // cone.glsl:38-46 at BLACK
       const V3 hit = v3s(0.0f) - P3(p, 0);
       const float h = p.a[3], rad = p.a[4];
-      const float tana = rad / h;
+      const float tana = fdiv(rad, h);
       const float dd = sqrtf_(hit.x * hit.x + hit.y * hit.y);
-      const float x1 = dd / tana, x2 = dd * tana;
+      const float x1 = fdiv(dd, tana), x2 = dd * tana;
       normal = s * normalize(hit - v3(0.0f, 0.0f, h - x1 - x2));
       return v3s(0.0f);
     }
@@ -869,7 +831,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
     }
     case SAIL_HYPERBOLOID: if (!HAS(c.kShapes, SAIL_HYPERBOLOID)) break; {
       const V3 hit = v3s(0.0f), p1 = P3(p, 3), p2 = P3(p, 6);
-      const float v = (hit.z - p1.z) / (p2.z - p1.z);
+      const float v = fdiv(hit.z - p1.z, p2.z - p1.z);
       const V3 pr = (1.0f - v) * p1 + v * p2;
       const float phi = phiOf(pr.x * hit.y - hit.x * pr.y, hit.x * pr.x + hit.y * pr.y);
       V3 dpdu, dpdv;
@@ -896,21 +858,21 @@ D float sinTheta(V3 w) { return sqrtf_(sin2Theta(w)); }
 D float tan2Theta(V3 w) {
   const float cos2T = w.z * w.z;
   if (cos2T < kEps) return kInf;
-  return sin2Theta(w) / cos2T;
+  return fdiv(sin2Theta(w), cos2T);
 }
-D float cosPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 1.0f : clamp_(w.x / st, -1.0f, 1.0f); }
-D float sinPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 0.0f : clamp_(w.y / st, -1.0f, 1.0f); }
+D float cosPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 1.0f : clamp_(fdiv(w.x, st), -1.0f, 1.0f); }
+D float sinPhi(V3 w) { const float st = sinTheta(w); return equalZero(st) ? 0.0f : clamp_(fdiv(w.y, st), -1.0f, 1.0f); }
 D bool sameHemisphere(V3 w, V3 wp) { return w.z * wp.z > kEps; }
 
 D float frDielectric(float cosThetaI, float etaI, float etaT) {
   cosThetaI = clamp_(cosThetaI, -1.0f, 1.0f);
   const float sinThetaI = sqrtf_(fmax_(0.0f, 1.0f - cosThetaI * cosThetaI));
-  const float sinThetaT = etaI / etaT * sinThetaI;
+  const float sinThetaT = fdiv(etaI, etaT) * sinThetaI;
   if (sinThetaT >= 1.0f) return 1.0f;
   const float cosThetaT = sqrtf_(fmax_(0.0f, 1.0f - sinThetaT * sinThetaT));
   const float TI = etaT * cosThetaI, IT = etaI * cosThetaT, II = etaI * cosThetaI, TT = etaT * cosThetaT;
-  const float Rparl = (TI - IT) / (TI + IT), Rperp = (II - TT) / (II + TT);
-  return (Rparl * Rparl + Rperp * Rperp) / 2.0f;
+  const float Rparl = fdiv(TI - IT, TI + IT), Rperp = fdiv(II - TT, II + TT);
+  return fdiv(Rparl * Rparl + Rperp * Rperp, 2.0f);
 }
 D V3 frConductor(float cosThetaI, V3 etaI, V3 etaT, V3 k) {
   cosThetaI = clamp_(cosThetaI, -1.0f, 1.0f);
@@ -940,16 +902,16 @@ D V3 frEvaluate(const Fr& f, float cosThetaI) {
 D V3 trSampleWh(V2 u, float ax, float ay, V3 wo) {  // microfacet.glsl:41-59
   float cosT = 0.0f, phi = 2.0f * kPI * u.x;
   if (ax == ay) {
-    const float tanTheta2 = ax * ax * u.x / (1.0f - u.x);
-    cosT = 1.0f / sqrtf_(1.0f + tanTheta2);
+    const float tanTheta2 = fdiv(ax * ax * u.x, 1.0f - u.x);
+    cosT = rcp_rn(sqrtf_(1.0f + tanTheta2));
   } else {
-    phi = atanf_(ay / ax * tanf_(kPiOver2 + 2.0f * kPI * u.x));
+    phi = atanf_(fdiv(ay, ax) * tanf_(kPiOver2 + 2.0f * kPI * u.x));
     if (u.x > 0.5f) phi += kPI;
     float sP, cP; sincosf_(phi, sP, cP);
     const float ax2 = ax * ax, ay2 = ay * ay;
-    const float alpha2 = 1.0f / (cP * cP / ax2 + sP * sP / ay2);
-    const float tanTheta2 = alpha2 * u.x / (1.0f - u.x);
-    cosT = 1.0f / sqrtf_(1.0f + tanTheta2);
+    const float alpha2 = rcp_rn(fdiv(cP * cP, ax2) + fdiv(sP * sP, ay2));
+    const float tanTheta2 = fdiv(alpha2 * u.x, 1.0f - u.x);
+    cosT = rcp_rn(sqrtf_(1.0f + tanTheta2));
   }
   const float sinT = sqrtf_(fmax_(0.0f, 1.0f - cosT * cosT));
   float sp, cp; sincosf_(phi, sp, cp);
@@ -963,8 +925,8 @@ D float trD(float ax, float ay, V3 wh) {  // microfacet.glsl:61-67
   const float c2 = wh.z * wh.z;
   const float cos4Theta = c2 * c2;
   const float cp = cosPhi(wh), sp = sinPhi(wh);
-  const float e = (cp * cp / (ax * ax) + sp * sp / (ay * ay)) * t2;
-  return 1.0f / (kPI * ax * ay * cos4Theta * (1.0f + e) * (1.0f + e));
+  const float e = (fdiv(cp * cp, ax * ax) + fdiv(sp * sp, ay * ay)) * t2;
+  return rcp_rn(kPI * ax * ay * cos4Theta * (1.0f + e) * (1.0f + e));
 }
 D float trPdf(float ax, float ay, V3 wh) { return trD(ax, ay, wh) * absCosTheta(wh); }
 D V3 microR_f(V3 R, const Fr& fr, float ax, float ay, V3 wo, V3 wi) {  // bsdf.glsl:168-178
@@ -981,34 +943,34 @@ D V3 microR_sample(V3 R, const Fr& fr, float ax, float ay, V2 u, V3 wo, V3& wi, 
   const V3 wh = trSampleWh(u, ax, ay, wo);
   wi = reflect_(-wo, wh);
   if (!sameHemisphere(wo, wi)) return v3s(0.0f);
-  pdf = trPdf(ax, ay, wh) / (4.0f * dot(wo, wh));
+  pdf = fdiv(trPdf(ax, ay, wh), 4.0f * dot(wo, wh));
   return microR_f(R, fr, ax, ay, wo, wi);
 }
 D V3 microT_f(V3 T, float etaB, bool into, float ax, float ay, V3 wo, V3 wi) {  // :205-224 (etaA = 1)
   if (sameHemisphere(wo, wi)) return v3s(0.0f);
   const float cosThetaO = wo.z, cosThetaI = wi.z;
   if (equalZero(cosThetaI) || equalZero(cosThetaO)) return v3s(0.0f);
-  const float eta = into ? (etaB / 1.0f) : (1.0f / etaB);
+  const float eta = into ? fdiv(etaB, 1.0f) : rcp_rn(etaB);
   V3 wh = normalize(wo + wi * eta);
   if (wh.z < -kEps) wh = -wh;
   const float Fd = frDielectric(dot(wo, wh), 1.0f, etaB);
   const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
   return (1.0f - Fd) * T *
-         fabsf(eta * eta * trD(ax, ay, wh) * fabsf(dot(wi, wh)) * fabsf(dot(wo, wh)) /
-               (cosThetaI * cosThetaO * sqrtDenom * sqrtDenom));
+         fabsf(fdiv(eta * eta * trD(ax, ay, wh) * fabsf(dot(wi, wh)) * fabsf(dot(wo, wh)),
+                    cosThetaI * cosThetaO * sqrtDenom * sqrtDenom));
 }
 D float microT_pdf(float etaB, bool into, float ax, float ay, V3 wo, V3 wi) {  // :226-235
   if (sameHemisphere(wo, wi)) return 0.001f;
-  const float eta = into ? (etaB / 1.0f) : (1.0f / etaB);
+  const float eta = into ? fdiv(etaB, 1.0f) : rcp_rn(etaB);
   const V3 wh = normalize(wo + wi * eta);
   const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
-  const float dwh_dwi = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
+  const float dwh_dwi = fabsf(fdiv(eta * eta * dot(wi, wh), sqrtDenom * sqrtDenom));
   return trPdf(ax, ay, wh) * dwh_dwi;
 }
 D V3 microT_sample(V3 T, float etaB, bool into, float ax, float ay, V2 u, V3 wo, V3& wi, float& pdf) {
   if (equalZero(wo.z)) return v3s(0.0f);
   const V3 wh = trSampleWh(u, ax, ay, wo);
-  const float eta = into ? (1.0f / etaB) : (etaB / 1.0f);
+  const float eta = into ? rcp_rn(etaB) : fdiv(etaB, 1.0f);
   wi = refract_(-wo, wh, eta);
   pdf = microT_pdf(etaB, into, ax, ay, wo, wi);
   return microT_f(T, etaB, into, ax, ay, wo, wi);
@@ -1022,8 +984,8 @@ D V3 orenNayar_f(V3 R, float A, float B, V3 wo, V3 wi) {  // bsdf.glsl:45-66
     maxCos = fmax_(0.0f, dCos);
   }
   float sinAlpha, tanBeta;
-  if (absCosTheta(wi) > absCosTheta(wo)) { sinAlpha = sinThetaO; tanBeta = sinThetaI / absCosTheta(wi); }
-  else { sinAlpha = sinThetaI; tanBeta = sinThetaO / absCosTheta(wo); }
+  if (absCosTheta(wi) > absCosTheta(wo)) { sinAlpha = sinThetaO; tanBeta = fdiv(sinThetaI, absCosTheta(wi)); }
+  else { sinAlpha = sinThetaI; tanBeta = fdiv(sinThetaO, absCosTheta(wo)); }
   return R * kInvPI * (A + B * maxCos * sinAlpha * tanBeta);
 }
 
@@ -1070,7 +1032,7 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
           fs = (kr * sc) / absCosTheta(wi);
         } else {
           const float etaI = ins.into ? 1.0f : eta, etaT = ins.into ? eta : 1.0f;
-          wi = refract_(-wo, v3(0.0f, 0.0f, 1.0f), etaI / etaT);
+          wi = refract_(-wo, v3(0.0f, 0.0f, 1.0f), fdiv(etaI, etaT));
           const V3 ft = (kt * sc) * (1.0f - Fd);
           pdf = 1.0f;
           fs = ft / absCosTheta(wi);
@@ -1139,7 +1101,7 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
       const float cT = -(-nt).y;
       if (cT < ctw) fall = 0.0f;
       else if (cT >= cfs) fall = 1.0f;
-      else { const float delta = (cT - ctw) / (cfs - ctw); const float d2 = delta * delta; fall = d2 * d2; }
+      else { const float delta = fdiv(cT - ctw, cfs - ctw); const float d2 = delta * delta; fall = d2 * d2; }
     }
     contrib = em * fall * fmax_(0.0f, dot(normalize(toLight), ins.normal)) / (d * d);
     lit = true;
@@ -1459,7 +1421,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       if (alive) {
         ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
         ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
-        ray.rx = ray.ry = ray.rz = 0.0;  // not used past the sweep: the next ray is rebuilt by mkRay
+        ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
         fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
         pixel = __float_as_int(sSt[9][li]);
         sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
@@ -1639,10 +1601,10 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
     const float col[3] = {cv.x, cv.y, cv.z};
     for (int c = 0; c < 3; c++) {
       if (A.kind == 0) o[c] = col[c];
-      else if (A.kind == 1) o[c] = powf_(col[c], 1.0f / A.gammaC);
+      else if (A.kind == 1) o[c] = powf_(col[c], rcp_rn(A.gammaC));
       else {
         const float xx = fmax_(0.0f, col[c] - 0.004f);
-        o[c] = (xx * (6.2f * xx + 0.5f)) / (xx * (6.2f * xx + 1.7f) + 0.06f);
+        o[c] = fdiv(xx * (6.2f * xx + 0.5f), xx * (6.2f * xx + 1.7f) + 0.06f);
       }
     }
   } else if (A.kind == 3) {  // window.glsl:1-44, FILTER_WINDOW_WIDTH 4
@@ -1650,8 +1612,8 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
     float weightSum = 0.0f;
     for (int i = 0; i < 4; i++) {
       for (int j = 0; j < 4; j++) {
-        const float wi = ((float)j + 0.5f) * A.rx / 4.0f, wj = ((float)i + 0.5f) * A.ry / 4.0f;
-        const float ox = wi / (float)A.W, oy = wj / (float)A.H;
+        const float wi = fdiv(((float)j + 0.5f) * A.rx, 4.0f), wj = fdiv(((float)i + 0.5f) * A.ry, 4.0f);
+        const float ox = fdiv(wi, (float)A.W), oy = fdiv(wj, (float)A.H);
         V3 tmp = v3s(0.0f);
         int count = 0;
         for (int q = 0; q < 4; q++) {
@@ -1666,7 +1628,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
         acc = acc + tmp * weight;
       }
     }
-    o[0] = acc.x / weightSum; o[1] = acc.y / weightSum; o[2] = acc.z / weightSum;
+    o[0] = fdiv(acc.x, weightSum); o[1] = fdiv(acc.y, weightSum); o[2] = fdiv(acc.z, weightSum);
   } else if (A.kind == 4) {  // wavelet.glsl:5-54 (edge-avoiding a-trous over the colour and position maps)
     const V3 cval = sample(A, A.accum, true, tcx, tcy);
     const V3 pval = sample(A, A.aovP, false, tcx, tcy);
@@ -1686,23 +1648,23 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
           float h = 0.0f;
           if (delt % div == 0) h = hk[(delt / div) % 5];
           if (h == 0.0f) continue;
-          const float u = (tcx - A.rx / dW) + ((float)j + 0.5f) * A.rx / dW2;
-          const float v = (tcy - A.ry / dH) + ((float)i + 0.5f) * A.ry / dH2;
+          const float u = (tcx - fdiv(A.rx, dW)) + fdiv(((float)j + 0.5f) * A.rx, dW2);
+          const float v = (tcy - fdiv(A.ry, dH)) + fdiv(((float)i + 0.5f) * A.ry, dH2);
           const V3 ctmp = sample(A, A.accum, true, u, v);
           const V3 t = cval - ctmp;
           const float tw = 1.0f - 1.0f;
-          const float c_w = fmin_(expf_(-(dot4(t, tw)) / 4.0f), 1.0f);
-          const float d2 = fmax_(dot4(t, tw) / (stepwidth * stepwidth), 0.0f);
-          const float n_w = fmin_(expf_(-(d2) / 128.0f), 1.0f);
+          const float c_w = fmin_(expf_(fdiv(-(dot4(t, tw)), 4.0f)), 1.0f);
+          const float d2 = fmax_(fdiv(dot4(t, tw), stepwidth * stepwidth), 0.0f);
+          const float n_w = fmin_(expf_(fdiv(-(d2), 128.0f)), 1.0f);
           const V3 tp = pval - sample(A, A.aovP, false, u, v);
-          const float p_w = fmin_(expf_(-(dot4(tp, tw)) / 1.0f), 1.0f);
+          const float p_w = fmin_(expf_(fdiv(-(dot4(tp, tw)), 1.0f)), 1.0f);
           const float weight = c_w * n_w * p_w * h;
           weightSum += weight;
           col[0] += ctmp.x * weight; col[1] += ctmp.y * weight; col[2] += ctmp.z * weight; col[3] += 1.0f * weight;
         }
       }
     }
-    for (int c = 0; c < 4; c++) o[c] = col[c] / weightSum;
+    for (int c = 0; c < 4; c++) o[c] = fdiv(col[c], weightSum);
   } else {  // normal.glsl / position.glsl: the AOV map at the texel
     const V3 m = sample(A, A.kind == 5 ? A.aovN : A.aovP, false, tcx, tcy);
     o[0] = m.x; o[1] = m.y; o[2] = m.z;
@@ -1752,7 +1714,8 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
     case 8: r = x[i] / y[i]; break;
     case 9: r = fmin_(x[i], y[i]); break;
     case 10: r = fmax_(x[i], y[i]); break;
-    case 11: r = xdiv(x[i], y[i], rcp_exact(y[i])); break;  // shared-reciprocal divide
+    case 11: r = fdiv(x[i], y[i]); break;  // GLSL divide spec
+    case 14: r = rcp_rn(x[i]); break;
     case 12: r = clamp_(x[i], 0.0f, 1.0f); break;
     default: break;
   }

@@ -57,13 +57,13 @@ def _args(fn, rng, n):
         x = np.concatenate([xs.ravel(), rng.normal(size=n).astype(np.float32)])
         y = np.concatenate([ys.ravel(), rng.normal(size=n).astype(np.float32)])
         return x, y
-    if fn == 11:  # shared-reciprocal divide vs IEEE divide over raw bit patterns (all classes)
+    if fn in (11, 14):  # GLSL divide a * RN(1/b) and its reciprocal over raw bit patterns (all classes)
         bits = rng.integers(0, 2 ** 32, (2, n), dtype=np.uint64).astype(np.uint32)
         return bits[0].view(np.float32), bits[1].view(np.float32)
     return rng.normal(size=n) * 100, rng.normal(size=n) * 10 ** rng.uniform(-5, 5, n)
 
 
-@pytest.mark.parametrize("fn", list(range(13)))
+@pytest.mark.parametrize("fn", list(range(13)) + [14])
 def test_math_spec_bit_exact(gpu, fn):
     rng = np.random.default_rng(1000 + fn)
     x, y = _args(fn, rng, 1 << 18)

@@ -184,3 +184,25 @@ def test_spec_math_accuracy(fn, ref, lo, hi):
     ulp = np.spacing(np.abs(want).astype(np.float32)).astype(np.float64)
     tol = 4.0 if fn == 2 else 2.0  # tan = sin/cos adds one rounding and amplifies near pi/2
     assert (np.abs(got - want) <= tol * ulp).all()
+
+
+def test_division_spec_within_glsl_bound():
+    """GLSL division a / b := a * RN(1/b) (ref_math.h div_s): within 1.5 ulp of the exact quotient over normal
+    results, inside GLSL ES 3.00's 2.5 ulp bound; RN(1/b) itself is the correctly rounded reciprocal"""
+    rng = np.random.default_rng(77)
+    a = (rng.normal(size=200000) * 10 ** rng.uniform(-15, 15, 200000)).astype(np.float32)
+    b = (rng.normal(size=200000) * 10 ** rng.uniform(-15, 15, 200000)).astype(np.float32)
+    got = oracle.math(11, a, b).astype(np.float64)
+    want = a.astype(np.float64) / b.astype(np.float64)
+    normal = (np.abs(want) > 1e-37) & (np.abs(want) < 1e37)
+    ulp = np.spacing(np.abs(want).astype(np.float32)).astype(np.float64)
+    assert (np.abs(got - want)[normal] <= 1.5 * ulp[normal]).all()
+    r = oracle.math(14, b).astype(np.float32)
+    assert np.array_equal(r.view(np.uint32), (np.float32(1.0) / b).view(np.uint32))
+    # exact when the divisor's reciprocal is exact (powers of two), and the same special values as IEEE
+    p2 = np.float32(2.0) ** rng.integers(-20, 20, 1000).astype(np.float32)
+    assert np.array_equal(oracle.math(11, a[:1000], p2), a[:1000] / p2)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0], np.float32)
+    xs, ys = np.meshgrid(sp, sp)
+    g, w = oracle.math(11, xs.ravel(), ys.ravel()), xs.ravel() / ys.ravel()
+    assert ((g.view(np.uint32) == w.view(np.uint32)) | (np.isnan(g) & np.isnan(w))).all()
