@@ -6,7 +6,7 @@ cd "$(dirname "$0")"
 mkdir -p lib build
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 ARCH=${SAIL_ARCH:-gfx950}
-COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function"
+COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function"
 $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_trace.hip -o build/sail_trace.o ${SAIL_EXTRA:-}
 $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_capi.cpp -o build/sail_capi.o
 $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_hostmath.cpp -o build/sail_hostmath.o

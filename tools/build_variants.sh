@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../sail_amd"
 mkdir -p lib/variants build/variants
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function --offload-arch=gfx950"
+COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-function --offload-arch=gfx950"
 $HIPCC $COMMON -c csrc/sail_capi.cpp -o build/variants/sail_capi.o
 $HIPCC $COMMON -c csrc/sail_hostmath.cpp -o build/variants/sail_hostmath.o
 while [ $# -ge 2 ]; do
