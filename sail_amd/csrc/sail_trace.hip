@@ -797,21 +797,21 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const V3 bhl = sw.bhl;
   Hit h;
   h.d = best;
-  h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
-  h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0;
-  if (bi < 0) return h;
+  // precondition: bi >= 0 is a sweep winner, so its shape is compiled into this kernel (primT returns
+  // MAX_DISTANCE for any other row, which never wins): no zero record is needed on any path -- a divergent
+  // zero default would be materialised for every lane before the dispatch
   const SailPrim& p = PRIM(c, bi);
   switch (p.type) {
-    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) cubeHit(c, p, r, best, h); break;
-    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) sphereHit(c, p, bhl, h); break;
-    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) rectHit(c, p, bhl, h); break;
-    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) coneHit(c, p, bhl, h); break;
-    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) cylinderHit(c, p, bhl, h); break;
-    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) diskHit(c, p, bhl, h); break;
-    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) hypHit(c, p, bhl, h); break;
-    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) paraHit(c, p, bhl, h); break;
-    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) cornellHit(p, r, best, h); break;
-    default: break;
+    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
+    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) { rectHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) { cylinderHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) { cornellHit(p, r, best, h); break; } __builtin_unreachable();
+    default: __builtin_unreachable();
   }
   h.matRow = p.matRow;
   h.emission = v3(p.em[0], p.em[1], p.em[2]);
@@ -837,6 +837,13 @@ D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
 D Hit intersectObjects(const Ctx& c, const Ray& r, PhaseClock& pc) {
   const Sweep sw = sweepRay(c, r);
   PHASE_MARK(pc, 0);  // primitive sweep
+  if (sw.bi < 0) {  // a miss: only d is read (the AOV store substitutes zeros)
+    Hit h;
+    h.d = sw.best;
+    h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
+    h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0;
+    return h;
+  }
   return hitRecord(c, r, sw);
 }
 
