@@ -105,6 +105,8 @@ struct sail_ctx {
   int32_t* lightObjRow = nullptr;
   SailSample* samples = nullptr;
   int samplesCap = 0;
+  int samplesPos = 0;  // ring position: each launch sequence reads its own slice of the sample buffer
+  SailSample* samplesPinned = nullptr;  // pinned host mirror of the ring (asynchronous uploads)
   std::vector<SailSample> hostSamples;
   std::vector<float> objectsRows;
   int n = 0, tn = 0, ln = 0;
@@ -221,7 +223,7 @@ int resetAccum(sail_ctx* c) {
   HIPCHK(c, hipMemsetAsync(c->accum, 0, bytes, c->stream));
   if (c->aovN) HIPCHK(c, hipMemsetAsync(c->aovN, 0, bytes, c->stream));
   if (c->aovP) HIPCHK(c, hipMemsetAsync(c->aovP, 0, bytes, c->stream));
-  if (c->segCounter) HIPCHK(c, hipMemsetAsync(c->segCounter, 0, sizeof(unsigned long long), c->stream));
+  if (c->segCounter) HIPCHK(c, hipMemsetAsync(c->segCounter, 0, SAIL_SEG_SLOTS * sizeof(unsigned long long), c->stream));
   int rc = collectEvents(c);
   if (rc) return rc;
   c->k = 0;
@@ -402,10 +404,13 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
 
 int ensureSamples(sail_ctx* c, int count) {
   if (count <= c->samplesCap) return SAIL_OK;
+  c->samplesPos = 0;
   if (c->samples) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->samples)); c->samples = nullptr; }
-  int cap = 64;
+  int cap = 4096;  // 256 KB: thousands of one-sample frames before the ring wraps
   while (cap < count) cap *= 2;
+  if (c->samplesPinned) { (void)hipHostFree(c->samplesPinned); c->samplesPinned = nullptr; }
   if (hipMalloc(&c->samples, sizeof(SailSample) * cap) != hipSuccess) return fail(c, SAIL_E_OOM, "sample buffer");
+  if (hipHostMalloc(&c->samplesPinned, sizeof(SailSample) * cap) != hipSuccess) c->samplesPinned = nullptr;
   c->samplesCap = cap;
   return SAIL_OK;
 }
@@ -416,9 +421,21 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   if (count <= 0 || owned <= 0) return SAIL_OK;
   int rc = ensureSamples(c, count);
   if (rc) return rc;
-  // the upload is ordered with the launch on the context stream
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->samples, hs, sizeof(SailSample) * count, hipMemcpyHostToDevice, c->stream));
+  // The upload is ordered with its launches on the context stream. Each call takes the next slice of a ring
+  // of sample records, so the host never waits for launches still reading earlier slices (one-sample frames
+  // from Renderer.render() queue back to back); only a wrap of the ring waits for the stream.
+  if (c->samplesPos + count > c->samplesCap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->samplesPos = 0;
+  }
+  SailSample* dev = c->samples + c->samplesPos;
+  const SailSample* src = hs;
+  if (c->samplesPinned) {  // staged in the pinned mirror: the copy is a true async DMA (pageable ones wait)
+    memcpy(c->samplesPinned + c->samplesPos, hs, sizeof(SailSample) * count);
+    src = c->samplesPinned + c->samplesPos;
+  }
+  c->samplesPos += count;
+  HIPCHK(c, hipMemcpyAsync(dev, src, sizeof(SailSample) * count, hipMemcpyHostToDevice, c->stream));
   const long long px = ownedPixels(c);
   for (int s0 = 0; s0 < count; s0 += c->launchSpp) {
     const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
@@ -426,7 +443,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     memset(&A, 0, sizeof A);
     A.prims = c->prims; A.typeMasks = reinterpret_cast<const unsigned long long*>(c->prims + c->n);
     A.texparams = c->tp; A.lights = c->lt; A.lightObjRow = c->lightObjRow;
-    A.samples = c->samples + s0;
+    A.samples = dev + s0;
     A.accum = c->accum; A.aovN = c->aovN; A.aovP = c->aovP; A.segCounter = c->segCounter;
     A.W = c->W; A.H = c->H; A.n = c->n; A.tn = c->tn; A.ln = c->ln;
     A.matMask = c->plugins.material_mask; A.texMask = c->plugins.texture_mask; A.lightMask = c->plugins.light_mask;
@@ -550,7 +567,7 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
     if (hipMalloc(&c->aovN, bytes) != hipSuccess || hipMalloc(&c->aovP, bytes) != hipSuccess) return bail(SAIL_E_OOM, "aov");
   }
   if (flags & SAIL_FLAG_SEGMENT_COUNT) {
-    if (hipMalloc(&c->segCounter, sizeof(unsigned long long)) != hipSuccess) return bail(SAIL_E_OOM, "counter");
+    if (hipMalloc(&c->segCounter, SAIL_SEG_SLOTS * sizeof(unsigned long long)) != hipSuccess) return bail(SAIL_E_OOM, "counter");
   }
   if (resetAccum(c) != SAIL_OK) return bail(SAIL_E_HIP, c->err.c_str());
   if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(SAIL_E_HIP, "sync");
@@ -567,6 +584,7 @@ void sail_destroy(sail_ctx* c) {
   for (auto e : c->evPool) (void)hipEventDestroy(e);
   void* bufs[] = {c->accum, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
   for (void* b : bufs) if (b) (void)hipFree(b);
+  if (c->samplesPinned) (void)hipHostFree(c->samplesPinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -842,9 +860,10 @@ int sail_get_stats(sail_ctx* c, sail_stats* s) {
   s->last_launch_ms = c->lastLaunchMs;
   s->launches = c->launches;
   if (c->segCounter) {
-    unsigned long long v = 0;
-    HIPCHK(c, hipMemcpy(&v, c->segCounter, sizeof v, hipMemcpyDeviceToHost));
-    s->segments = v;
+    unsigned long long v[SAIL_SEG_SLOTS];
+    HIPCHK(c, hipMemcpy(v, c->segCounter, sizeof v, hipMemcpyDeviceToHost));
+    s->segments = 0;
+    for (int i = 0; i < SAIL_SEG_SLOTS; i++) s->segments += v[i];
   }
   return SAIL_OK;
 }

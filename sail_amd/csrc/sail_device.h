@@ -48,7 +48,7 @@ struct SailTraceArgs {
   float4* accum;            // W x H, row 0 = bottom
   float4* aovN;             // optional
   float4* aovP;             // optional
-  unsigned long long* segCounter;  // optional exact segment counter
+  unsigned long long* segCounter;  // optional exact segment counter: SAIL_SEG_SLOTS partial sums
   float eye[3];
   int W, H;
   int n, tn, ln;
@@ -73,6 +73,8 @@ struct SailTraceArgs {
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a
 // set's masks may use that set's kernel; everything else runs the generic one.
 enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
+// the exact segment counter is kept as this many partial sums (spread atomics), added on readback
+#define SAIL_SEG_SLOTS 64
 #define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))
 #define SAIL_KSET_CORNELL_MATS ((1u << SAIL_MATTE) | (1u << SAIL_MIRROR))
 #define SAIL_KSET_CORNELL_TEX 0u

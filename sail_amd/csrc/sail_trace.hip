@@ -1362,10 +1362,11 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
     for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
 #endif
   if (A.segCounter) {
-    // one atomic per wave: sum the lanes' segment counts with a cross-lane reduction
+    // one atomic per wave: sum the lanes' segment counts with a cross-lane reduction; the waves spread their
+    // atomics over kSegSlots counters (one address took ~0.2 ms per 1080p launch in contended atomics)
     unsigned long long v = segs;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) atomicAdd(A.segCounter, v);
+    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
   }
 }
 // Path compaction: after every primitive sweep the workgroup's 256 live paths are sorted through LDS by
@@ -1534,7 +1535,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (A.segCounter) {
     unsigned long long v = segs;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) atomicAdd(A.segCounter, v);
+    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
   }
 }
 // Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;

@@ -15,18 +15,20 @@ function args() {
   return o;
 }
 
-function cornell() {
+function cornell(o) {
   const scene = new Sail.Scene();
   scene.add(new Sail.Cube([2.13, 5.487, 2.27], [3.43, 5.488, 3.32], new Sail.Matte(0.7),
     Sail.Color.createTexture([0, 0, 0]), [8, 8, 8]));
   scene.add(new Sail.Cornellbox([0, 0, -7], [5.560, 5.488, 5.592]));
   scene.add(new Sail.Sphere([2, 1.25, 2.70], 1.2, new Sail.Mirror(1.0), Sail.Color.WHITE));
-  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  const cam = new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]);
+  cam.makePerspective(55, o.width / o.height, 1, 100);  // the C2 view (SURVEY §8(d)); the reference passes aspect 1
+  scene.add(cam);
   return scene;
 }
 
 function run(o, perFrame) {
-  const scene = cornell();
+  const scene = cornell(o);
   const r = new Sail.Renderer({ width: o.width, height: o.height, maxBounces: o.bounces, deterministic: true,
     accumulation: 'sum', aov: false, display: false });
   r.update(scene);
