@@ -109,6 +109,7 @@ struct sail_ctx {
   SailSample* samplesPinned = nullptr;  // pinned host mirror of the ring (asynchronous uploads)
   std::vector<SailSample> hostSamples;
   std::vector<float> objectsRows;
+  std::vector<float> tpRows;  // host copy of texParams (category words of updated objects)
   int n = 0, tn = 0, ln = 0;
   sail_plugins plugins{};
   bool haveScene = false;
@@ -334,6 +335,17 @@ void primBoundsHost(SailPrim& p) {
     lo[k] -= pad; hi[k] += pad;
   }
   for (int k = 0; k < 3; k++) { p.a[18 + k] = (float)lo[k]; p.a[21 + k] = (float)hi[k]; }
+}
+
+// the category words the kernel tests (material.glsl / texture dispatch: int(readFloat(row, 0))), clamped to
+// [-1, 32] (every test is == c, < 0 or >= 32 against categories in [0, 31]) and packed in SailPrim.cats
+void fillCats(std::vector<SailPrim>& prims, const float* texparams, int tn) {
+  auto cat = [&](int row) {
+    const int v = (tn > 0 && row >= 0 && row < tn) ? to_int(texparams[(size_t)row * 16]) : 0;
+    return v < -1 ? -1 : (v > 32 ? 32 : v);
+  };
+  for (SailPrim& p : prims)
+    p.cats = (int32_t)(((uint32_t)(uint16_t)(int16_t)cat(p.matRow)) | ((uint32_t)(uint16_t)(int16_t)cat(p.texRow) << 16));
 }
 
 void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk) {
@@ -619,6 +631,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   c->plugins = *plugins;
   std::vector<SailPrim> prims;
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit);
+  fillCats(prims, texparams, tn);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -643,6 +656,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   HIPCHK(c, hipMemcpyAsync(c->lightObjRow, lrow.data(), rb, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->objectsRows.assign(objects, objects + (size_t)n * 18);
+  c->tpRows.assign(texparams, texparams + (size_t)tn * 16);
   c->n = n; c->tn = tn; c->ln = ln;
   c->haveScene = true;
   return resetAccum(c);
@@ -654,6 +668,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<SailPrim> prims;
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit);
+  fillCats(prims, c->tpRows.data(), c->tn);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -24,7 +24,8 @@ struct __attribute__((aligned(16))) SailPrim {
   int32_t matRow;   // texParams row of the material (Cornellbox: slot 7 quirk resolved here)
   int32_t texRow;   // texParams row of the texture
   float em[3];      // emission (Cornellbox: forced BLACK, cornellbox.glsl:19)
-  float pad0;
+  int32_t cats;     // int() of the material / texture category words (texParams[row][0]) clamped to [-1, 32]:
+                    // low / high 16 bits (host-evaluated; every category test reads the same answer)
   float a[24];      // shape parameters in row order, per-scene constants, a[18..23] padded bounds (sail_capi.cpp)
 };
 

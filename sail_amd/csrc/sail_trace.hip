@@ -212,9 +212,11 @@ D V2 concentricSampleDisk(V2 u) {
 
 // ---- textures (shader.texture.js:22-29) ----------------------------------------------------------------
 // UNIFORM_COLOR ignores uv, so hit records skip the UV arithmetic (atan2/acos/divides) for it
-D bool needsUV(const Ctx& c, int texRow) { return to_int(TP(c, texRow, 0)) != SAIL_TEX_UNIFORM; }
-D V3 getSurfaceColor(const Ctx& c, V2 uv, int texRow) {
-  const int cat = to_int(TP(c, texRow, 0));
+D int matCat(const SailPrim& p) { return (int)(short)(p.cats & 0xffff); }
+D int texCat(const SailPrim& p) { return p.cats >> 16; }
+D bool needsUV(const SailPrim& p) { return texCat(p) != SAIL_TEX_UNIFORM; }
+D V3 getSurfaceColor(const Ctx& c, V2 uv, const SailPrim& p) {
+  const int texRow = p.texRow, cat = texCat(p);
   if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
   if (cat < 0 || cat >= 32 || !((c.texMask >> cat) & 1u)) return v3s(0.0f);
   switch (cat) {
@@ -306,14 +308,14 @@ D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
   h.normal = normalForCube(r.o + t * r.d, p);
   dpdBox(h.normal, h.dpdu, h.dpdv);
   V2 uv = v2(0.0f, 0.0f);
-  if (needsUV(c, p.texRow)) {
+  if (needsUV(p)) {
     const V3 mn = P3(p, 0), mx = P3(p, 3);
     const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
     if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(fdiv(hh.y, tr.y), fdiv(hh.z, tr.z));
     else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(fdiv(hh.x, tr.x), fdiv(hh.z, tr.z));
     else uv = v2(fdiv(hh.x, tr.x), fdiv(hh.y, tr.y));
   }
-  h.sc = getSurfaceColor(c, uv, p.texRow);
+  h.sc = getSurfaceColor(c, uv, p);
 }
 D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
   h.hit = r.o + t * r.d;
@@ -366,7 +368,7 @@ D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   // theta of the UV and of computeDpDForSphere (:33-43) are the same value: the pole guard touches x only
   const float theta = acosf_(clamp_(fdiv(hl.z, rad), -1.0f, 1.0f));
   V2 uv = v2(0.0f, 0.0f);
-  if (needsUV(c, p.texRow)) {
+  if (needsUV(p)) {
     V3 hit = hl;
     if (hit.x == 0.0f && hit.y == 0.0f) hit.x = 1e-5f * rad;
     uv = v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(theta, kPI));
@@ -378,7 +380,7 @@ D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const V3 dpdu = dpduRot(hl);
   const V3 dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(th2));
   const V3 nl = normalize(cross(dpdv, dpdu));
-  h.sc = getSurfaceColor(c, uv, p.texRow);
+  h.sc = getSurfaceColor(c, uv, p);
   h.hit = L2W(hl) + P3(p, 0);
   h.normal = L2W(nl);
   h.dpdu = L2W(dpdu);
@@ -411,7 +413,7 @@ D float rectT(const SailPrim& p, const Ray& r, V3* hitOut) {
 D void rectHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const RectFrame f = rectFrame(p);
   h.dpdu = f.dpdu; h.dpdv = f.dpdv; h.normal = f.normal;
-  h.sc = getSurfaceColor(c, needsUV(c, p.texRow) ? v2(fdiv(hl.x, f.maxX), fdiv(hl.y, f.maxY)) : v2(0.0f, 0.0f), p.texRow);
+  h.sc = getSurfaceColor(c, needsUV(p) ? v2(fdiv(hl.x, f.maxX), fdiv(hl.y, f.maxY)) : v2(0.0f, 0.0f), p);
   h.hit = localToWorld(hl, f.normal, f.ss, f.ts) + P3(p, 0);
 }
 
@@ -538,7 +540,7 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
 // local-space tail shared by the quadrics and the disk: normal from dpdu x dpdv, texture, back to world
 D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dpdv, Hit& h) {
   const V3 nl = normalize(cross(dpdu, dpdv));
-  h.sc = getSurfaceColor(c, uv, p.texRow);
+  h.sc = getSurfaceColor(c, uv, p);
   h.hit = L2W(hl) + P3(p, 0);
   h.normal = L2W(nl);
   h.dpdu = L2W(dpdu);
@@ -546,14 +548,14 @@ D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dp
 }
 D void coneHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
-  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
+  const V2 uv = needsUV(p) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
   const float vv = fdiv(hit.z, hh);
   const V3 dpdv = v3(fdiv(-hit.x, 1.0f - vv), fdiv(-hit.y, 1.0f - vv), hh);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
 D void cylinderHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float hh = p.a[3];
-  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
+  const V2 uv = needsUV(p) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z, hh)) : v2(0.0f, 0.0f);
   finishLocal(c, p, hit, uv, dpduRot(hit), v3(0.0f, 0.0f, hh), h);
 }
 D void hypDpD(V3 hit, V3 p1, V3 p2, float phi, V3& dpdu, V3& dpdv) {  // hyperboloid.glsl:41-46
@@ -577,7 +579,7 @@ D void paraDpD(V3 hit, float zMax, float zMin, V3& dpdu, V3& dpdv) {  // parabol
 }
 D void paraHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
-  const V2 uv = needsUV(c, p.texRow) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z - zMin, zMax - zMin)) : v2(0.0f, 0.0f);
+  const V2 uv = needsUV(p) ? v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), fdiv(hit.z - zMin, zMax - zMin)) : v2(0.0f, 0.0f);
   V3 dpdu, dpdv;
   paraDpD(hit, zMax, zMin, dpdu, dpdv);
   finishLocal(c, p, hit, uv, dpdu, dpdv, h);
@@ -586,7 +588,7 @@ D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const float rad = p.a[3], ri = p.a[4];
   const float dist2 = hit.x * hit.x + hit.y * hit.y;
   V2 uv = v2(0.0f, 0.0f);
-  if (needsUV(c, p.texRow)) {
+  if (needsUV(p)) {
     const float rHit = sqrtf_(dist2);
     const float oneMinusV = fdiv(rHit - ri, rad - ri);
     uv = v2(fdiv(phiOf(hit.y, hit.x), 2.0f * kPI), 1.0f - oneMinusV);
@@ -817,7 +819,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   h.emission = v3(p.em[0], p.em[1], p.em[2]);
   const V3 nn = sgn(p.rev) * h.normal;                       // faceObj test (shader.shape.js:47-49)
   if (!(dot(nn, r.d) < -kEps)) h.emission = v3s(0.0f);
-  h.matCategory = to_int(TP(c, h.matRow, 0));
+  h.matCategory = matCat(p);
   h.into = dot(h.normal, r.d) < -kEps;
   if (!h.into) h.normal = -h.normal;
   return h;
@@ -1462,7 +1464,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           key = 1 + sw.bi;
         } else {
           const SailPrim& p = PRIM(c, sw.bi);
-          int mc = to_int(TP(c, p.matRow, 0));
+          int mc = matCat(p);
           mc = (mc >= 0 && mc < 5) ? mc : 0;
           key = 1 + p.type * 5 + mc;
         }
