@@ -350,3 +350,38 @@ def test_sample_groups(gpu, fixtures, monkeypatch, name, groups, mode):
     assert bit_equal(got, want).all()
     assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
     assert st.segments == segs
+
+
+# ---- category words outside the compiled sets (unknown, negative, NaN, huge): the zero material / texture paths,
+# through the host-evaluated SailPrim.cats -------------------------------------------------------------------------
+def test_odd_category_words(gpu, fixtures):
+    sc = dict(fixtures["scenes"]["ALL"])
+    tp = list(sc["texparams"])
+    odd = [99.0, -5.0, float("nan"), 3e9, 31.0]
+    for i, row in enumerate(range(0, sc["tn"], 2)):
+        tp[row * 16] = odd[i % len(odd)]
+    sc["texparams"] = tp
+    got, want, st, segs, _, _ = _render_both({"scenes": {"ODD": sc}}, "ODD", 24, 20, 3, 6, launch=2)
+    assert bit_equal(got, want).all()
+    assert st.segments == segs
+
+
+# ---- one sample per call (Renderer.render): the sample-record ring wraps after 4096 calls ---------------------------
+def test_single_sample_frames_ring_wrap(gpu, fixtures):
+    sc = fixtures["scenes"]["C1"]
+    W, H, B, spp = 8, 6, 4, 4100
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    ctx = capi.Context(W, H, flags=capi.FLAG_SEGMENT_COUNT)
+    try:
+        ctx.set_scene_dict(sc)
+        for k in range(spp):
+            ctx.render(inv[k], sc["eye"], float(seeds[k]), B)
+        got = ctx.read_accum()
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    oracle.reset_counters()
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    segs, _ = oracle.counters()
+    assert bit_equal(got, want).all()
+    assert st.segments == segs and st.launches == spp
