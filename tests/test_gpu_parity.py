@@ -51,7 +51,7 @@ def _args(fn, rng, n):
         return rng.normal(size=n) * 10 ** rng.uniform(-3, 3, n), None
     if fn == 7:  # ordinary magnitudes plus raw bit patterns (negative, zero, subnormal, inf, NaN, huge)
         bits = rng.integers(0, 2 ** 32, n // 2, dtype=np.uint64).astype(np.uint32).view(np.float32)
-        return np.concatenate([np.abs(rng.normal(size=n // 2)) * 10 ** rng.uniform(-10, 10, n // 2), bits]), None
+        return np.concatenate([(np.abs(rng.normal(size=n // 2)) * 10 ** rng.uniform(-10, 10, n // 2)).astype(np.float32), bits]), None
     if fn in (9, 10, 12):  # min / max / clamp: signed zeros, NaN, inf and ordinary values, every pairing
         special = np.array([0.0, -0.0, 1.0, -1.0, np.nan, np.inf, -np.inf, 0.5, 2.0, -1e-30], np.float32)
         xs, ys = np.meshgrid(special, special)
