@@ -270,6 +270,9 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                # the op model counts every add/mul/min/max/divide/transcendental as one op: its ceiling is one op
+                # per lane per cycle (the FP32 peak above counts an FMA as two), so this is the pipe's fraction
+                "frac_one_op_per_lane": round(achieved_tflops / (FP32_PEAK_TFLOPS / 2), 4),
                 "ops_per_segment": round(ops_seg, 2), "kernel": ctx.kernel_name(),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
