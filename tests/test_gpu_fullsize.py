@@ -3,6 +3,7 @@ render: oracle-rendered crops of the same frame (bit-exact), finiteness / sample
 tile split emulated on one device summing to the 1-rank frame bit for bit."""
 import json
 import os
+import zlib
 
 import numpy as np
 import pytest
@@ -42,11 +43,11 @@ def test_full_frame_crops_match_oracle(frozen, cfg, name, W, H, B, spp):
     ctx.close()
     assert np.isfinite(got).all()
     assert (got[..., 3] == spp).all()
-    rng = np.random.default_rng(hash(cfg) % 2 ** 32)
+    rng = np.random.default_rng(zlib.crc32(cfg.encode()))  # deterministic crops (str hash is salted)
     masks = capi.plugin_masks(sc["plugins"])
     c = 8
     crops = [(0, 0), (W - c, H - c), (W // 2 - c // 2, H // 2 - c // 2)] + \
-            [(int(rng.integers(0, W - c)), int(rng.integers(0, H - c))) for _ in range(5)]
+            [(int(rng.integers(0, W - c)), int(rng.integers(0, H - c))) for _ in range(12)]
     for x0, y0 in crops:
         want = np.zeros((H, W, 4), np.float32)
         oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=want)
