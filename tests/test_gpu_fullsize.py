@@ -71,3 +71,21 @@ def test_c2_eight_rank_split_equals_single_rank(frozen):
     full = ctx.read_accum()
     ctx.close()
     assert _bits_equal(total, full)
+
+
+def test_c4_precull_conservative_full_frame(frozen, monkeypatch):
+    """the padded-box pre-cull only skips rows that cannot win: the full C4 frame with and without it is the same
+    bit for bit (every pixel, 2 samples, 12 bounces; tools/cull_check.py)"""
+    sc = frozen["C4"]
+    W, H, B, spp = 3840, 2160, 12, 2
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    out = {}
+    for cull in ("0", "1000"):
+        monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+        ctx = capi.Context(W, H)
+        ctx.set_scene_dict(sc)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        out[cull] = ctx.read_accum()
+        ctx.close()
+    assert _bits_equal(out["0"], out["1000"])
