@@ -385,3 +385,38 @@ def test_single_sample_frames_ring_wrap(gpu, fixtures):
     segs, _ = oracle.counters()
     assert bit_equal(got, want).all()
     assert st.segments == segs and st.launches == spp
+
+
+# ---- degenerate rays through the division spec's fallback paths: exactly axis-aligned directions (zero and
+# negative-zero components: reciprocals +-inf), origins on primitive planes, subnormal / huge components --------
+def _degenerate_rays(sc, rng):
+    objs = np.array(sc["objects"], np.float32).reshape(sc["n"], 18)
+    pts = [objs[i, 1:4] for i in range(sc["n"])] + [objs[i, 4:7] for i in range(sc["n"])]  # row coordinates
+    pts += [np.array(sc["eye"], np.float32)]
+    dirs = []
+    for ax in range(3):
+        for s in (1.0, -1.0):
+            d = np.zeros(3, np.float32); d[ax] = s; dirs.append(d)
+            d2 = np.array([-0.0, -0.0, -0.0], np.float32); d2[ax] = s; dirs.append(d2)
+    dirs += [np.array([1e-39, 1.0, 0.0], np.float32), np.array([3e38, 1e-3, -2.0], np.float32),
+             np.array([0.0, 0.0, 0.0], np.float32), np.array([1.0, 1.0, 0.0], np.float32)]
+    rays = []
+    for p in pts:
+        for d in dirs:
+            rays.append(np.concatenate([p, d]))
+            jit = p + rng.normal(size=3).astype(np.float32) * np.float32(0.25)
+            rays.append(np.concatenate([jit, d]))
+    return np.array(rays, np.float32)
+
+
+@pytest.mark.parametrize("name", ["C1", "C3", "C4", "ALL"])
+def test_pick_degenerate_rays(gpu, fixtures, name):
+    sc = fixtures["scenes"][name]
+    rays = _degenerate_rays(sc, np.random.default_rng(11))
+    ctx = capi.Context(8, 8)
+    ctx.set_scene_dict(sc)
+    idx, t = ctx.pick(rays)
+    ctx.close()
+    widx, wt = oracle.pick(sc, capi.plugin_masks(sc["plugins"])[0], rays)
+    assert np.array_equal(idx, widx)
+    assert bit_equal(t, wt).all()
