@@ -420,3 +420,23 @@ def test_pick_degenerate_rays(gpu, fixtures, name):
     widx, wt = oracle.pick(sc, capi.plugin_masks(sc["plugins"])[0], rays)
     assert np.array_equal(idx, widx)
     assert bit_equal(t, wt).all()
+
+
+# ---- unusual viewpoints: inside the mirror sphere, on the light's plane, in a Cornell-box corner, looking straight
+# along an axis (primary rays with exact zero components), outside the closed box --------------------------------
+VIEWS = [("inside sphere", [2.0, 1.25, 2.7], [2.78, 2.73, 2.79]),
+         ("light plane", [2.78, 5.487, 2.8], [2.78, 0.0, 3.3]),
+         ("corner", [0.0, 0.0, -7.0], [5.56, 5.488, 5.592]),
+         ("axis", [2.78, 2.73, -6.0], [2.78, 2.73, 5.0]),
+         ("outside", [2.78, 2.73, -20.0], [2.78, 2.73, 2.79])]
+
+
+@pytest.mark.parametrize("label,eye,center", VIEWS)
+def test_unusual_viewpoints(gpu, fixtures, label, eye, center):
+    sc = dict(fixtures["scenes"]["C1"])
+    sc["eye"] = eye
+    sc["mvp_rowmajor"] = capi.camera(eye, center, [0, 1, 0], 55.0, 1.0, 1.0, 100.0).tolist()
+    got, want, st, segs, gaov, waov = _render_both({"scenes": {"V": sc}}, "V", 33, 21, 3, 6, aov=True, launch=2)
+    assert bit_equal(got, want).all(), label
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all(), label
+    assert st.segments == segs, label
