@@ -49,10 +49,11 @@ def load_scene(name="C1"):
         return json.load(f)[name]
 
 
-def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0):
+def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1):
     """BASELINE.json's CPU baseline: the single-threaded JS/Node software shader (oracle/sail_soft.js, bit-exact
     with the C++ oracle and the HIP kernel) timed on the host on a bounded sample of the same frame: 32x32
-    crops spiralling out from the centre, 8 spp each, until ~budget_s of render time (node start excluded)."""
+    crops spiralling out from the centre, 8 spp each, until ~budget_s of render time (node start excluded).
+    threads > 1: the same shader on that many worker_threads, crops dealt round-robin (SURVEY §8(d) optional)."""
     import shutil
     import subprocess
     import tempfile
@@ -62,13 +63,13 @@ def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0):
     spp, c = 8, 32
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     cx, cy = (W - c) // 2, (H - c) // 2
-    offsets = sorted(((dx, dy) for dx in range(-9, 10) for dy in range(-9, 10)), key=lambda d: d[0] ** 2 + d[1] ** 2)
+    offsets = sorted(((dx, dy) for dx in range(-30, 31) for dy in range(-17, 18)), key=lambda d: d[0] ** 2 + d[1] ** 2)
     crops = [[cx + dx * c, cy + dy * c, c, c] for dx, dy in offsets
              if 0 <= cx + dx * c and 0 <= cy + dy * c and cx + dx * c + c <= W and cy + dy * c + c <= H]
     job = {"objects": sc["objects"], "n": sc["n"], "texparams": sc["texparams"], "tn": sc["tn"], "lights": sc["lights"],
            "ln": sc["ln"], "masks": list(masks), "W": W, "H": H, "inv": [float(v) for v in inv.reshape(-1)],
            "seeds": [float(v) for v in seeds], "eye": sc["eye"], "spp": spp, "maxBounces": B, "accumMode": 0,
-           "crops": crops, "budgetSeconds": budget_s}
+           "crops": crops, "budgetSeconds": budget_s, "threads": threads}
     with tempfile.TemporaryDirectory() as td:
         jp = os.path.join(td, "job.json")
         with open(jp, "w") as f:
@@ -76,8 +77,9 @@ def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0):
         out = subprocess.run([node, os.path.join(ROOT, "oracle", "sail_soft.js"), jp, os.path.join(td, "o")],
                              capture_output=True, text=True, timeout=budget_s * 10 + 60, check=True).stdout
     r = json.loads(out.strip().splitlines()[-1])
-    return {"value": r["segments"] / r["seconds"] / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "implementation": f"oracle/sail_soft.js on Node {r['node']}, single thread",
+    return {"value": r["segments"] / r["seconds"] / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "implementation": f"oracle/sail_soft.js on Node {r['node']}, "
+                              + ("single thread" if threads == 1 else f"{threads} worker_threads"),
             "sample": f"{r['crops']} centre-out {c}x{c} crops of the frame, {spp} spp x {B} bounces = {r['segments']} "
                       f"segments (exact count) in {r['seconds']:.2f} s"}
 
@@ -291,7 +293,9 @@ def main():
             # the north star's JS/Node software shader; the C++ restatement is timed beside it for reference
             cpp = cpu_baseline(sc, masks, mvp, W, H, B, budget_s=5.0)
             js = cpu_baseline_js(sc, masks, mvp, W, H, B)
-            rec["cpu_baseline"] = dict(js, cpp_port=cpp) if js else cpp
+            nthr = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16 cores
+            jsmt = cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=6.0, threads=nthr) if (js and nthr > 1) else None
+            rec["cpu_baseline"] = dict(js, cpp_port=cpp, worker_threads=jsmt) if js else cpp
         print(json.dumps(rec), flush=True)
     ctx.close()
     if dist is not None:

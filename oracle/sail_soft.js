@@ -1117,29 +1117,55 @@ function mathFn(fn, x, y) {
 module.exports = { render, mathFn, fma32 };
 
 // CLI: node oracle/sail_soft.js job.json out_prefix -> out_prefix.accum.f32 (+ .aovn/.aovp) and a JSON line
-if (require.main === module) {
+// timed baseline: render crops in order until the time budget is spent (one thread, or worker `w` of `nw`
+// taking crops w, w + nw, ...)
+function timedCrops(job, w = 0, nw = 1) {
+  const accum = new Float32Array(job.W * job.H * 4);
+  let segments = 0, done = 0, sec = 0;
+  const t0 = process.hrtime.bigint();
+  for (let i = w; i < job.crops.length; i += nw) {
+    segments += render(Object.assign({}, job, { crop: job.crops[i], accum })).segments;
+    done++;
+    sec = Number(process.hrtime.bigint() - t0) / 1e9;
+    if (sec >= job.budgetSeconds) break;
+  }
+  return { segments, seconds: sec, crops: done };
+}
+
+let wt = null;
+try { wt = require('worker_threads'); } catch (e) { wt = null; }
+if (wt && !wt.isMainThread && wt.workerData && wt.workerData.sailCrops) {
+  const d = wt.workerData;
+  wt.parentPort.postMessage(timedCrops(d.job, d.w, d.nw));
+} else if (require.main === module) {
   const fs = require('fs');
   const [jobPath, outPrefix] = process.argv.slice(2);
   const job = JSON.parse(fs.readFileSync(jobPath, 'utf8'));
-  if (job.math !== undefined) {  // {math: fn, xHex, yHex: little-endian f32 arrays as hex} -> f32 results
+  if (job.crops && job.threads > 1 && wt) {  // the same shader on job.threads worker threads
+    const nw = job.threads;
+    const t0 = process.hrtime.bigint();
+    let left = nw, segments = 0, crops = 0;
+    for (let w = 0; w < nw; w++) {
+      const worker = new wt.Worker(__filename, { workerData: { sailCrops: true, job, w, nw } });
+      worker.on('message', (r) => {
+        segments += r.segments; crops += r.crops;
+        if (--left === 0) {
+          const sec = Number(process.hrtime.bigint() - t0) / 1e9;
+          process.stdout.write(JSON.stringify({ segments, seconds: sec, crops, threads: nw, node: process.version }) + '\n');
+        }
+      });
+      worker.on('error', (e) => { process.stderr.write(String(e) + '\n'); process.exitCode = 1; });
+    }
+  } else if (job.math !== undefined) {  // {math: fn, xHex, yHex: little-endian f32 arrays as hex} -> f32 results
     const hex = (h) => { const b = Buffer.from(h, 'hex'); return new Float32Array(b.buffer.slice(b.byteOffset, b.byteOffset + b.length)); };
     const x = hex(job.xHex), y = hex(job.yHex);
     const out = new Float32Array(x.length);
     for (let i = 0; i < out.length; i++) out[i] = mathFn(job.math, x[i], y[i]);
     fs.writeFileSync(outPrefix + '.math.f32', Buffer.from(out.buffer));
     process.stdout.write(JSON.stringify({ n: out.length }) + '\n');
-  } else if (job.crops) {  // timed baseline: render crops in order until the time budget is spent
-    const accum = new Float32Array(job.W * job.H * 4);
-    let segments = 0, done = 0;
-    const t0 = process.hrtime.bigint();
-    let sec = 0;
-    for (const crop of job.crops) {
-      segments += render(Object.assign({}, job, { crop, accum })).segments;
-      done++;
-      sec = Number(process.hrtime.bigint() - t0) / 1e9;
-      if (sec >= job.budgetSeconds) break;
-    }
-    process.stdout.write(JSON.stringify({ segments, seconds: sec, crops: done, node: process.version }) + '\n');
+  } else if (job.crops) {
+    const r = timedCrops(job);
+    process.stdout.write(JSON.stringify({ segments: r.segments, seconds: r.seconds, crops: r.crops, node: process.version }) + '\n');
   } else {
     if (job.accumB64) job.accum = new Float32Array(Buffer.from(job.accumB64, 'base64').buffer.slice(0));
     const t0 = process.hrtime.bigint();
