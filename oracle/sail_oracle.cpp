@@ -10,7 +10,8 @@
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
 //
 // Defined semantics for what GLSL leaves open: uninitialised locals and unwritten `out`
-// parameters are 0; min/max/clamp return the non-NaN operand; transcendentals follow ref_math.h;
+// parameters are 0; min/max/clamp return the non-NaN operand; transcendentals follow ref_math.h; GLSL division
+// a / b is a * RN(1/b) (ref_math.h div_s: the reciprocal-multiply form GPU compilers emit, correctly rounded);
 // int() truncates (NaN -> 0); negative % follows C; a NaN texture row coordinate addresses row 0;
 // a zero-height texture reads 0. Floating-point contraction is disabled at build time.
 //
