@@ -116,6 +116,8 @@ struct sail_ctx {
   int shadowAnyHit = 0;
   std::vector<unsigned long long> typeMasksHost;  // staging for the per-chunk type masks (async copy source)
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
+  int cullFma = 1;       // SAIL_CULL_FMA=0: always the plain pre-cull form (tests)
+  double primExtent = INFINITY;  // largest |padded bound| coordinate (inf: some primitive is unbounded)
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int numCUs = 256;
@@ -337,6 +339,23 @@ void primBoundsHost(SailPrim& p) {
   for (int k = 0; k < 3; k++) { p.a[18 + k] = (float)lo[k]; p.a[21 + k] = (float)hi[k]; }
 }
 
+// Largest padded-bound coordinate of the scene, inf when a primitive has no finite bound. Every ray origin
+// is the eye or a hit point inside some padded box, so |origin| <= max(extent, |eye|) (see cullFmaOk).
+double primExtent(const std::vector<SailPrim>& prims) {
+  double m = 0.0;
+  for (const SailPrim& p : prims)
+    for (int k = 18; k < 24; k++) m = fmax(m, std::isfinite(p.a[k]) ? fabs((double)p.a[k]) : INFINITY);
+  return m;
+}
+
+// The fused pre-cull form (sail_trace.hip padHitF) tests each slab plane as fma(a, R, -RN(o R)): the plane
+// lands within |o| 2^-24 of where the plain (a - o) R puts it, so the test stays conservative while that is
+// far inside the 1e-3 padding. |o| < 4096 keeps it under 2.5e-4; it also keeps o R finite with R <= 1e30.
+bool cullFmaOk(const sail_ctx* c) {
+  const double e = fmax(fmax(fabs(c->eyeCache[0]), fabs(c->eyeCache[1])), fabs(c->eyeCache[2]));
+  return c->cullFma && fmax(c->primExtent, e) < 4096.0;
+}
+
 // the category words the kernel tests (material.glsl / texture dispatch: int(readFloat(row, 0))), clamped to
 // [-1, 32] (every test is == c, < 0 or >= 32 against categories in [0, 31]) and packed in SailPrim.cats
 void fillCats(std::vector<SailPrim>& prims, const float* texparams, int tn) {
@@ -465,7 +484,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.rank = (c->partMode == SAIL_PART_SAMPLES) ? 0 : c->rank;
     A.ownedTiles = owned;
     A.shadowAnyHit = c->shadowAnyHit;
-    A.cullPrims = c->n >= c->cullMinPrims;
+    A.cullPrims = c->n >= c->cullMinPrims ? (cullFmaOk(c) ? 2 : 1) : 0;
     A.kernelSet = kernelSetFor(c);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
@@ -561,6 +580,7 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
   c->device = device; c->W = width; c->H = height; c->flags = flags;
   if (const char* e = getenv("SAIL_CULL_MIN_PRIMS")) c->cullMinPrims = atoi(e);  // tests force the pre-cull on/off
   if (const char* e = getenv("SAIL_FORCE_GENERIC")) c->forceGeneric = atoi(e);
+  if (const char* e = getenv("SAIL_CULL_FMA")) c->cullFma = atoi(e);
   if (const char* e = getenv("SAIL_SAMPLE_GROUPS")) c->forceGroups = atoi(e);
   auto bail = [&](int code, const char* what) {
     g_create_error = std::string("sail_create: ") + what;
@@ -632,6 +652,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   std::vector<SailPrim> prims;
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit);
   fillCats(prims, texparams, tn);
+  c->primExtent = primExtent(prims);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -669,6 +690,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   std::vector<SailPrim> prims;
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit);
   fillCats(prims, c->tpRows.data(), c->tn);
+  c->primExtent = primExtent(prims);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));

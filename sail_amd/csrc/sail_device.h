@@ -61,7 +61,8 @@ struct SailTraceArgs {
   int world, rank;          // tile partition: global tile t belongs to rank t % world
   int ownedTiles;           // tiles of this rank
   int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
-  int cullPrims;            // 1: padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test
+  int cullPrims;            // padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test:
+                            // 1 plain slab form, 2 fused form (host-checked scene extent, sail_capi.cpp cullFmaOk)
   int kernelSet;            // SAIL_KSET_*: the precompiled plugin-set kernel to launch
   // sample groups (small per-rank frames): sampleGroups workgroups share each 16x16 block, group g renders
   // samples [g*groupSpp, (g+1)*groupSpp) into stage[k * stageStride + slot]; sail_accum_kernel then adds them

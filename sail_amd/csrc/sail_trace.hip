@@ -155,6 +155,7 @@ struct Ctx {
   float fcx, fcy;
   int shadowAnyHit;
   int cullPrims;
+  int cullFma;     // the candidate sweep's pre-cull in the fused form (padHitF)
   // plugin sets compiled into this kernel instantiation (compile-time constants after inlining): the
   // reference generates one GLSL program per scene plugin set (shader.js combinefs); this build precompiles
   // kernels for plugin subsets and dispatches the smallest one that covers the scene
@@ -675,9 +676,39 @@ D void cullStat(bool pass) {
 // candidate masks built from descending rows shifted into two 32-bit halves (one select + one v_lshl_or per
 // row instead of a 64-bit shift, two moves, two selects and two ors): C4 +2.7 %. Packing the x/y slab
 // arithmetic of padHit into v_pk_add_f32 / v_pk_mul_f32 (SAIL_CULL_PK) was measured at -3.4 %.
-#ifndef SAIL_CULL_MASK2
-#define SAIL_CULL_MASK2 1
-#endif
+// Fused pre-cull form (A.cullPrims == 2): each slab plane as fma(a, R, -RN(o R)), 2 FMAs per axis instead of
+// 2 subtractions + 2 multiplies, o R hoisted per ray. Against the plain form each plane moves by at most
+// |o| 2^-24 (the host enables it only while that is far inside the padding: sail_capi.cpp cullFmaOk). The
+// reciprocals are clamped to +-1e30 first: for an axis-parallel ray (R = +-inf) the plain form gives the
+// slab (+-inf, +-inf) while a R - o R would be inf - inf = NaN, which min/max then drop from one side only
+// (measured: 1.4 M rays of one C4 frame culled wrongly without the clamp). NaN reciprocals stay NaN.
+struct CullRay { float rx, ry, rz, ox, oy, oz; };
+D float clampRcp(float v) { return fabsf(v) > 1e30f ? __builtin_copysignf(1e30f, v) : v; }
+D CullRay cullRay(const Ray& r) {
+  CullRay q;
+  q.rx = clampRcp(r.rx); q.ry = clampRcp(r.ry); q.rz = clampRcp(r.rz);
+  q.ox = -(r.o.x * q.rx); q.oy = -(r.o.y * q.ry); q.oz = -(r.o.z * q.rz);
+  return q;
+}
+D bool padHitF(const SailPrim& p, const CullRay& q, float best) {
+  const float x0 = fma_(p.a[18], q.rx, q.ox), x1 = fma_(p.a[21], q.rx, q.ox);
+  const float y0 = fma_(p.a[19], q.ry, q.oy), y1 = fma_(p.a[22], q.ry, q.oy);
+  const float z0 = fma_(p.a[20], q.rz, q.oz), z1 = fma_(p.a[23], q.rz, q.oz);
+  const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
+  const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
+  return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > best * 1.0001f + 1e-4f);
+}
+// one 64-row chunk's candidate mask: descending rows shifted into two 32-bit halves (one select and one
+// v_lshl_or per row)
+template <bool FUSED>
+D unsigned long long chunkMask(const Ctx& c, const Ray& r, const CullRay& q, int base, int cnt, float bound) {
+  unsigned lo = 0u, hi = 0u;
+#define SWEEP_TEST(j) (FUSED ? padHitF(PRIM(c, base + (j)), q, bound) : CULL_TEST(c, PRIM(c, base + (j)), r, bound))
+  for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (SWEEP_TEST(j) ? 1u : 0u);
+  for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = (lo << 1) | (SWEEP_TEST(j) ? 1u : 0u);
+#undef SWEEP_TEST
+  return ((unsigned long long)hi << 32) | lo;
+}
 template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
   if constexpr (T == SAIL_CUBE) return cubeT(p, r);
   else if constexpr (T == SAIL_SPHERE) return sphereT(p, r, hl);
@@ -710,22 +741,12 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
 }
 // limit: the pre-cull distance bound before any hit (kMaxDistance, or 1 for shadow rays: see closestT)
 D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, V3& bhl) {
+  const CullRay q = cullRay(r);
   for (int base = 0; base < c.n; base += 64) {
     const int cnt = c.n - base < 64 ? c.n - base : 64;
     const float bound = fmin_(best, limit);
-    unsigned long long cand = 0ull;
-#if SAIL_CULL_MASK2
-    {  // descending rows shifted into two 32-bit halves: one select and one v_lshl_or per row
-      unsigned lo = 0u, hi = 0u;
-      for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (CULL_TEST(c, PRIM(c, base + j), r, bound) ? 1u : 0u);
-      for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--)
-        lo = (lo << 1) | (CULL_TEST(c, PRIM(c, base + j), r, bound) ? 1u : 0u);
-      cand = ((unsigned long long)hi << 32) | lo;
-    }
-#else
-    for (int j = 0; j < cnt; j++)
-      if (CULL_TEST(c, PRIM(c, base + j), r, bound)) cand |= 1ull << j;
-#endif
+    const unsigned long long cand =
+        c.cullFma ? chunkMask<true>(c, r, q, base, cnt, bound) : chunkMask<false>(c, r, q, base, cnt, bound);
     candType<SAIL_CUBE>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_CORNELLBOX>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_RECTANGLE>(c, r, base, cand, best, bi, bhl);
@@ -1325,6 +1346,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
   c.shadowAnyHit = A.shadowAnyHit;
   c.cullPrims = CULL ? 1 : 0;
+  c.cullFma = CULL && A.cullPrims == 2;
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   const size_t pix = (size_t)y * A.W + x;
@@ -1410,6 +1432,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.fcx = 0.0f; c.fcy = 0.0f;
   c.shadowAnyHit = A.shadowAnyHit;
   c.cullPrims = CULL ? 1 : 0;
+  c.cullFma = CULL && A.cullPrims == 2;
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   if (li < kKeys) sCnt[li] = 0;

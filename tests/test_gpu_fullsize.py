@@ -73,9 +73,13 @@ def test_c2_eight_rank_split_equals_single_rank(frozen):
     assert _bits_equal(total, full)
 
 
-def test_c4_precull_conservative_full_frame(frozen, monkeypatch):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_c4_precull_conservative_full_frame(frozen, monkeypatch, fused):
     """the padded-box pre-cull only skips rows that cannot win: the full C4 frame with and without it is the same
-    bit for bit (every pixel, 2 samples, 12 bounces; tools/cull_check.py)"""
+    bit for bit (every pixel, 2 samples, 12 bounces; tools/cull_check.py), in the fused slab form the library
+    picks for this scene and in the plain form (SAIL_CULL_FMA=0). C4's bounce rays include about 1.4 M
+    axis-parallel ones per sample (a zero direction component, infinite reciprocal)."""
+    monkeypatch.setenv("SAIL_CULL_FMA", fused)
     sc = frozen["C4"]
     W, H, B, spp = 3840, 2160, 12, 2
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Full-frame check that the pre-cull is conservative: the C4 frame (3840x2160, 12 bounces) rendered with the
 pre-cull kernel and with the pre-cull disabled (SAIL_CULL_MIN_PRIMS=1000: the in-order sweep over every row)
-must be bit-identical. Usage: tools/cull_check.py [spp]"""
+must be bit-identical. Usage: tools/cull_check.py [spp] [library .so, default the in-tree build]"""
 import json
 import os
 import sys
@@ -15,6 +15,8 @@ from sail_amd import capi  # noqa: E402
 
 def main():
     spp = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    if len(sys.argv) > 2:
+        capi._lib = capi.load(sys.argv[2])
     sc = json.load(open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")))["C4"]
     W, H, B = 3840, 2160, 12
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
