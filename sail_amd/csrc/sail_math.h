@@ -167,7 +167,13 @@ SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }
 SM_D float rcp_rn(float b) {
   if (__builtin_constant_p(b)) return 1.0f / b;
   const float ab = __builtin_fabsf(b);
-  if (__builtin_expect(!(ab >= 0x1p-126f && ab <= 0x1p126f), 0)) return 1.0f / b;
+  // the IEEE fallback sits behind a real branch: an empty volatile asm on its input keeps the compiler from
+  // if-converting it (the select form ran the ~12-instruction IEEE divide at every call; C2 +0.8 %)
+  if (__builtin_expect(!(ab >= 0x1p-126f && ab <= 0x1p126f), 0)) {
+    float bb = b;
+    __asm__ volatile("" : "+v"(bb));
+    return 1.0f / bb;
+  }
   const float y0 = __builtin_amdgcn_rcpf(b);
   return fma_(fma_(-b, y0, 1.0f), y0, y0);
 }
