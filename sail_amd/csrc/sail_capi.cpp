@@ -89,6 +89,9 @@ struct TexView {
 
 }  // namespace
 
+// union of the primitives' finite bounds and its diagonal (sceneBox)
+struct SceneBox { double lo[3], hi[3]; double diag; };
+
 struct sail_ctx {
   int device = 0, W = 0, H = 0;
   uint32_t flags = 0;
@@ -118,6 +121,7 @@ struct sail_ctx {
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
   int cullFma = 1;       // SAIL_CULL_FMA=0: always the plain pre-cull form (tests)
   double primExtent = INFINITY;  // largest |padded bound| coordinate (inf: some primitive is unbounded)
+  SceneBox scene{};              // union of the primitives' finite bounds (padPrimBounds)
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int numCUs = 256;
@@ -282,9 +286,12 @@ void quadricHost(SailPrim& p) {
 // pre-cull before the exact per-primitive test: a primitive whose padded box the ray misses, or enters
 // beyond the closest distance so far, cannot change the sweep's result (n = 67).
 // Local frames: OBJECT_SPACE maps world (x, y, z) -> local (-z, x, y), so the local z axis is world y.
-void primBoundsHost(SailPrim& p) {
+struct PrimBox { double lo[3], hi[3]; };
+PrimBox primBoundsRaw(const SailPrim& p) {
   const double inf = INFINITY;
-  double lo[3] = {-inf, -inf, -inf}, hi[3] = {inf, inf, inf};
+  PrimBox b{{-inf, -inf, -inf}, {inf, inf, inf}};
+  double* lo = b.lo;
+  double* hi = b.hi;
   const float* a = p.a;
   auto box = [&](double x0, double y0, double z0, double x1, double y1, double z1) {
     lo[0] = fmin(x0, x1); lo[1] = fmin(y0, y1); lo[2] = fmin(z0, z1);
@@ -331,12 +338,65 @@ void primBoundsHost(SailPrim& p) {
     }
     default: break;
   }
-  for (int k = 0; k < 3; k++) {
-    if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) { lo[k] = -inf; hi[k] = inf; continue; }
-    const double pad = 1e-3 + 1e-4 * fmax(fabs(lo[k]), fabs(hi[k]));
-    lo[k] -= pad; hi[k] += pad;
+  for (int k = 0; k < 3; k++)
+    if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) { lo[k] = -inf; hi[k] = inf; }
+  return b;
+}
+
+// Union of the primitives' finite bounds: every hit point, hence every bounce / shadow ray origin, lies in it.
+SceneBox sceneBox(const std::vector<PrimBox>& raw) {
+  SceneBox s{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}, 0.0};
+  bool any = false;
+  for (const PrimBox& b : raw) {
+    if (!std::isfinite(b.lo[0]) || !std::isfinite(b.lo[1]) || !std::isfinite(b.lo[2])) continue;
+    any = true;
+    for (int k = 0; k < 3; k++) { s.lo[k] = fmin(s.lo[k], b.lo[k]); s.hi[k] = fmax(s.hi[k], b.hi[k]); }
   }
-  for (int k = 0; k < 3; k++) { p.a[18 + k] = (float)lo[k]; p.a[21 + k] = (float)hi[k]; }
+  if (!any) { for (int k = 0; k < 3; k++) s.lo[k] = s.hi[k] = 0.0; }
+  s.diag = sqrt((s.hi[0] - s.lo[0]) * (s.hi[0] - s.lo[0]) + (s.hi[1] - s.lo[1]) * (s.hi[1] - s.lo[1]) +
+                (s.hi[2] - s.lo[2]) * (s.hi[2] - s.lo[2]));
+  return s;
+}
+
+// Padding of each primitive's bounds into a[18..23]. The exact f32 tests (the reference's GLSL) can report a hit
+// slightly outside the true surface, the more so the farther the ray origin: a slab / plane distance is off by
+// about L 2^-23 at range L, and a quadric's discriminant b^2 - 4ac loses about 20 L^2 2^-24 to cancellation,
+// which moves its hit band by that over the local radius (and by its square root near a cone apex or where the
+// radius is unknown). Origins here are hit points inside the scene box, or the eye when it lies within one
+// scene diagonal D of the box (sail_launch: cullPrimary), so L = 2D bounds every origin-to-primitive distance.
+// Padding = 1e-3 + 1e-4 |bound| + 2^-20 L, plus 1.2e-6 L^2 / r for quadrics (+ 1.1e-3 L for cones,
+// hyperboloids and paraboloids). Measured by the far-origin tests (tests/test_gpu_fullsize.py).
+void padPrimBounds(std::vector<SailPrim>& prims, const std::vector<PrimBox>& raw, const SceneBox& sb) {
+  const double L = 2.0 * sb.diag, kQ = 20.0 / 16777216.0;
+  for (size_t i = 0; i < prims.size(); i++) {
+    SailPrim& p = prims[i];
+    const PrimBox& b = raw[i];
+    double extra = L / 1048576.0;
+    double r = -1.0;  // local radius of a quadric (its smallest), -1: not a quadric
+    bool apex = false;
+    switch (p.type) {
+      case SAIL_SPHERE: r = fabs(p.a[3]); break;
+      case SAIL_CYLINDER: r = fabs(p.a[4]); break;
+      case SAIL_CONE: r = fabs(p.a[4]); apex = true; break;
+      case SAIL_HYPERBOLOID: case SAIL_PARABOLOID:
+        r = 0.5 * fmin(b.hi[0] - b.lo[0], b.hi[2] - b.lo[2]); apex = true; break;
+      default: break;
+    }
+    if (r >= 0.0) {
+      extra += (r > 0.0 && std::isfinite(r)) ? kQ * L * L / r : INFINITY;
+      if (apex) extra += sqrt(kQ) * L;
+    }
+    for (int k = 0; k < 3; k++) {
+      double lo = b.lo[k], hi = b.hi[k];
+      if (std::isfinite(lo) && std::isfinite(hi) && std::isfinite(extra)) {
+        const double pad = 1e-3 + 1e-4 * fmax(fabs(lo), fabs(hi)) + extra;
+        lo -= pad; hi += pad;
+      } else {
+        lo = -INFINITY; hi = INFINITY;
+      }
+      p.a[18 + k] = (float)lo; p.a[21 + k] = (float)hi;
+    }
+  }
 }
 
 // Largest padded-bound coordinate of the scene, inf when a primitive has no finite bound. Every ray origin
@@ -356,6 +416,18 @@ bool cullFmaOk(const sail_ctx* c) {
   return c->cullFma && fmax(c->primExtent, e) < 4096.0;
 }
 
+// Primary rays may use the pre-cull only when the eye lies within one scene diagonal of the scene box: the
+// padding (padPrimBounds) covers origin-to-primitive distances up to two diagonals.
+int eyeNearScene(const sail_ctx* c) {
+  double d2 = 0.0;
+  for (int k = 0; k < 3; k++) {
+    const double e = c->eyeCache[k];
+    const double g = e < c->scene.lo[k] ? c->scene.lo[k] - e : (e > c->scene.hi[k] ? e - c->scene.hi[k] : 0.0);
+    d2 += g * g;
+  }
+  return d2 == d2 && sqrt(d2) <= c->scene.diag;
+}
+
 // the category words the kernel tests (material.glsl / texture dispatch: int(readFloat(row, 0))), clamped to
 // [-1, 32] (every test is == c, < 0 or >= 32 against categories in [0, 31]) and packed in SailPrim.cats
 void fillCats(std::vector<SailPrim>& prims, const float* texparams, int tn) {
@@ -367,7 +439,9 @@ void fillCats(std::vector<SailPrim>& prims, const float* texparams, int tn) {
     p.cats = (int32_t)(((uint32_t)(uint16_t)(int16_t)cat(p.matRow)) | ((uint32_t)(uint16_t)(int16_t)cat(p.texRow) << 16));
 }
 
-void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk) {
+void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::vector<SailPrim>& out, int* anyHitOk,
+                 SceneBox* sbOut) {
+  std::vector<PrimBox> raw((size_t)n);
   TexView o{objects, 18, n};
   const float L = 17.0f;
   out.assign((size_t)n, SailPrim{});
@@ -426,11 +500,14 @@ void decodePrims(const float* objects, int n, int tn, uint32_t shapeMask, std::v
     }
     p.em[0] = v3[0]; p.em[1] = v3[1]; p.em[2] = v3[2];
     quadricHost(p);
-    primBoundsHost(p);
+    raw[i] = primBoundsRaw(p);
     // only slabs return t > EPSILON strictly; anything else may tie or undercut EPSILON, so shadow
     // rays must then find the true closest distance (shader.light.js:24-31)
     if (cat != SAIL_CUBE && cat != SAIL_CORNELLBOX) *anyHitOk = 0;
   }
+  const SceneBox sb = sceneBox(raw);
+  padPrimBounds(out, raw, sb);
+  if (sbOut) *sbOut = sb;
 }
 
 int ensureSamples(sail_ctx* c, int count) {
@@ -485,6 +562,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.ownedTiles = owned;
     A.shadowAnyHit = c->shadowAnyHit;
     A.cullPrims = c->n >= c->cullMinPrims ? (cullFmaOk(c) ? 2 : 1) : 0;
+    A.cullPrimary = eyeNearScene(c);
     A.kernelSet = kernelSetFor(c);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
@@ -650,7 +728,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->plugins = *plugins;
   std::vector<SailPrim> prims;
-  decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit);
+  decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
   c->primExtent = primExtent(prims);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
@@ -688,7 +766,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   if (n != c->n || !objects) return fail(c, SAIL_E_INVALID, "sail_update_objects: n must stay %d", c->n);
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<SailPrim> prims;
-  decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit);
+  decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, c->tpRows.data(), c->tn);
   c->primExtent = primExtent(prims);
   HIPCHK(c, hipStreamSynchronize(c->stream));

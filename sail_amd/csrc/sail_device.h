@@ -63,6 +63,7 @@ struct SailTraceArgs {
   int shadowAnyHit;         // 1 when no primitive can return d <= EPSILON (any-hit shadow rays are exact)
   int cullPrims;            // padded-box f32 pre-cull (SailPrim.a[18..23]) before each exact primitive test:
                             // 1 plain slab form, 2 fused form (host-checked scene extent, sail_capi.cpp cullFmaOk)
+  int cullPrimary;          // 1: primary rays use the pre-cull too (the eye is near the scene: eyeNearScene)
   int kernelSet;            // SAIL_KSET_*: the precompiled plugin-set kernel to launch
   // sample groups (small per-rank frames): sampleGroups workgroups share each 16x16 block, group g renders
   // samples [g*groupSpp, (g+1)*groupSpp) into stage[k * stageStride + slot]; sail_accum_kernel then adds them

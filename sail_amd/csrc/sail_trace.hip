@@ -156,6 +156,7 @@ struct Ctx {
   int shadowAnyHit;
   int cullPrims;
   int cullFma;     // the candidate sweep's pre-cull in the fused form (padHitF)
+  int cullPrimary; // primary rays may use the pre-cull (the eye is near the scene)
   // plugin sets compiled into this kernel instantiation (compile-time constants after inlining): the
   // reference generates one GLSL program per scene plugin set (shader.js combinefs); this build precompiles
   // kernels for plugin subsets and dispatches the smallest one that covers the scene
@@ -616,7 +617,7 @@ D float primT(const Ctx& c, const SailPrim& p, const Ray& r, V3* hl) {
 }
 
 // Cheap conservative pre-cull: the ray against the primitive's padded bounds in f32 (sail_capi.cpp
-// primBoundsHost). It rejects only rays that miss the padded box or enter it beyond the closest distance so
+// padPrimBounds). It rejects only rays that miss the padded box or enter it beyond the closest distance so
 // far (with margin); such a primitive's exact test could only return a miss or a larger distance.
 #if SAIL_CULL_PK
 typedef float sf2 __attribute__((ext_vector_type(2)));
@@ -786,12 +787,14 @@ D float closestT(const Ctx& c, const Ray& r) {
 // generated intersectObjects (shader.shape.js:28-51), split in two: one sweep keeps the winner's distance and
 // local hit point, then one full record is built for the winner alone
 struct Sweep { float best; int bi; V3 bhl; };
-D Sweep sweepRay(const Ctx& c, const Ray& r) {
+// primary: a camera ray, pre-culled only when the eye is near the scene (SailTraceArgs.cullPrimary)
+D Sweep sweepRay(const Ctx& c, const Ray& r, bool primary) {
   float best = kMaxDistance;
   int bi = -1;
   V3 bhl = v3s(0.0f);
+  const bool cull = c.cullPrims && (!primary || c.cullPrimary);
 #if SAIL_CAND_SWEEP
-  if (c.cullPrims) {
+  if (cull) {
     candSweep(c, r, kMaxDistance, best, bi, bhl);
     Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
     return sw;
@@ -799,7 +802,7 @@ D Sweep sweepRay(const Ctx& c, const Ray& r) {
 #endif
 #if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
+    if (cull && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
     V3 hl = v3s(0.0f);
     const float t = primT(c, PRIM(c, i), r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
@@ -857,8 +860,8 @@ D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
 #endif
   return hitRecord(c, r, sw);
 }
-D Hit intersectObjects(const Ctx& c, const Ray& r, PhaseClock& pc) {
-  const Sweep sw = sweepRay(c, r);
+D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc) {
+  const Sweep sw = sweepRay(c, r, primary);
   PHASE_MARK(pc, 0);  // primitive sweep
   if (sw.bi < 0) {  // a miss: only d is read (the AOV store substitutes zeros)
     Hit h;
@@ -1216,7 +1219,7 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, float4* aovN, float4*
   V3 fpdf = v3s(1.0f), e = v3s(0.0f);
   for (int depth = 1; depth <= maxDepth; depth++) {
     segs++;
-    const Hit ins = intersectObjects(c, ray, pc);
+    const Hit ins = intersectObjects(c, ray, depth == 1, pc);
     PHASE_MARK(pc, 1);  // hit record of the winner
     const float seed = tss + (float)depth;
     if (depth == 1 && aovPix >= 0) {
@@ -1347,6 +1350,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.shadowAnyHit = A.shadowAnyHit;
   c.cullPrims = CULL ? 1 : 0;
   c.cullFma = CULL && A.cullPrims == 2;
+  c.cullPrimary = A.cullPrimary;
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   const size_t pix = (size_t)y * A.W + x;
@@ -1433,6 +1437,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.shadowAnyHit = A.shadowAnyHit;
   c.cullPrims = CULL ? 1 : 0;
   c.cullFma = CULL && A.cullPrims == 2;
+  c.cullPrimary = A.cullPrimary;
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
   if (li < kKeys) sCnt[li] = 0;
@@ -1474,7 +1479,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int key = 0;
       if (alive) {
         segs++;
-        sw = sweepRay(c, ray);
+        sw = sweepRay(c, ray, depth == 1);
         if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
           if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
             const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);

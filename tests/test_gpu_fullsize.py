@@ -93,3 +93,55 @@ def test_c4_precull_conservative_full_frame(frozen, monkeypatch, fused):
         out[cull] = ctx.read_accum()
         ctx.close()
     assert _bits_equal(out["0"], out["1000"])
+
+
+
+def _far_eye(sc):
+    ctr = np.array(sc["center"], np.float64)
+    d = np.array(sc["eye"], np.float64) - ctr
+    sc["eye"] = [float(v) for v in ctr + d * (6000.0 / np.linalg.norm(d))]
+    o = np.array(sc["objects"], np.float32).reshape(-1, 18)
+    assert o[0, 0] == 1  # row 0: the room cube [0,0,-1]..[10,10,10] would hide the scene from outside:
+    o[0, 1:7] = [0.0, 0.0, 11.0, 10.0, 10.0, 12.0]  # keep only a back wall behind it
+    sc["objects"] = [float(v) for v in o.ravel()]
+    return 0.1  # field of view (degrees) that still frames the scene
+
+
+def _big_room(sc):
+    o = np.array(sc["objects"], np.float32).reshape(-1, 18)
+    assert o[0, 0] == 1  # row 0: the room cube [0,0,-1]..[10,10,10]
+    o[0, 1:4] -= 500.0
+    o[0, 4:7] += 500.0
+    sc["objects"] = [float(v) for v in o.ravel()]
+    return 55.0
+
+
+@pytest.mark.parametrize("variant", ["far_eye", "big_room"])
+def test_c4_precull_far_origins(frozen, monkeypatch, variant):
+    """ray origins far from the primitives: the eye 6,000 units away (primary rays), or the C4 room grown to
+    1,010 units a side (bounce rays leaving its walls). The reference's f32 quadric tests lose accuracy there
+    (discriminant cancellation grows with the squared distance), so the padded pre-cull must still pass every
+    row such a test can report as hit: with and without the pre-cull the frame is the same bit for bit, and
+    it matches oracle crops"""
+    sc = dict(frozen["C4"])
+    fov = _far_eye(sc) if variant == "far_eye" else _big_room(sc)
+    W, H, B, spp = 320, 180, 12, 2
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], fov, W / H, 1.0, 10000.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    out = {}
+    for cull in ("0", "1000"):
+        monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+        ctx = capi.Context(W, H)
+        ctx.set_scene_dict(sc)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        out[cull] = ctx.read_accum()
+        ctx.close()
+    got = out["0"]
+    assert got[..., :3].any()
+    assert _bits_equal(out["0"], out["1000"]), int((out["0"] != out["1000"]).any(axis=2).sum())
+    masks = capi.plugin_masks(sc["plugins"])
+    c = 8
+    for x0, y0 in [(W // 2 - c // 2, H // 2 - c // 2), (W // 3, H // 3), (0, 0)]:
+        want = np.zeros((H, W, 4), np.float32)
+        oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=want)
+        assert _bits_equal(got[y0:y0 + c, x0:x0 + c], want[y0:y0 + c, x0:x0 + c]), (x0, y0)
