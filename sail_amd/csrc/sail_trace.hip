@@ -691,20 +691,22 @@ D CullRay cullRay(const Ray& r) {
   q.ox = -(r.o.x * q.rx); q.oy = -(r.o.y * q.ry); q.oz = -(r.o.z * q.rz);
   return q;
 }
-D bool padHitF(const SailPrim& p, const CullRay& q, float best) {
+// B = best * 1.0001 + 1e-4 (> 0), computed once per chunk by the caller
+D bool padHitF(const SailPrim& p, const CullRay& q, float B) {
   const float x0 = fma_(p.a[18], q.rx, q.ox), x1 = fma_(p.a[21], q.rx, q.ox);
   const float y0 = fma_(p.a[19], q.ry, q.oy), y1 = fma_(p.a[22], q.ry, q.oy);
   const float z0 = fma_(p.a[20], q.rz, q.oz), z1 = fma_(p.a[23], q.rz, q.oz);
   const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
   const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
-  return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > best * 1.0001f + 1e-4f);
+  return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > B);
 }
 // one 64-row chunk's candidate mask: descending rows shifted into two 32-bit halves (one select and one
 // v_lshl_or per row)
 template <bool FUSED>
 D unsigned long long chunkMask(const Ctx& c, const Ray& r, const CullRay& q, int base, int cnt, float bound) {
   unsigned lo = 0u, hi = 0u;
-#define SWEEP_TEST(j) (FUSED ? padHitF(PRIM(c, base + (j)), q, bound) : CULL_TEST(c, PRIM(c, base + (j)), r, bound))
+  const float B = bound * 1.0001f + 1e-4f;
+#define SWEEP_TEST(j) (FUSED ? padHitF(PRIM(c, base + (j)), q, B) : CULL_TEST(c, PRIM(c, base + (j)), r, bound))
   for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (SWEEP_TEST(j) ? 1u : 0u);
   for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = (lo << 1) | (SWEEP_TEST(j) ? 1u : 0u);
 #undef SWEEP_TEST
