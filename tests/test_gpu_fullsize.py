@@ -116,15 +116,27 @@ def _big_room(sc):
     return 55.0
 
 
-@pytest.mark.parametrize("variant", ["far_eye", "big_room"])
+def _tiny_quadrics(sc):
+    o = np.array(sc["objects"], np.float32).reshape(-1, 18)
+    sph = o[:, 0] == 2  # Sphere rows: 2, c3, r (slot 4)
+    qd = (o[:, 0] == 4) | (o[:, 0] == 5)  # Cone / Cylinder rows: id, p3, h, r (slot 5)
+    assert sph.any() and qd.any()
+    o[sph, 4] *= 0.01
+    o[qd, 5] *= 0.01
+    sc["objects"] = [float(v) for v in o.ravel()]
+    return 55.0
+
+
+@pytest.mark.parametrize("variant", ["far_eye", "big_room", "tiny_quadrics"])
 def test_c4_precull_far_origins(frozen, monkeypatch, variant):
-    """ray origins far from the primitives: the eye 6,000 units away (primary rays), or the C4 room grown to
-    1,010 units a side (bounce rays leaving its walls). The reference's f32 quadric tests lose accuracy there
+    """ray origins far from the primitives: the eye 6,000 units away (primary rays), the C4 room grown to
+    1,010 units a side (bounce rays leaving its walls), or spheres, cones and cylinders shrunk 100x (origins
+    many radii away). The reference's f32 quadric tests lose accuracy there
     (discriminant cancellation grows with the squared distance), so the padded pre-cull must still pass every
     row such a test can report as hit: with and without the pre-cull the frame is the same bit for bit, and
     it matches oracle crops"""
     sc = dict(frozen["C4"])
-    fov = _far_eye(sc) if variant == "far_eye" else _big_room(sc)
+    fov = {"far_eye": _far_eye, "big_room": _big_room, "tiny_quadrics": _tiny_quadrics}[variant](sc)
     W, H, B, spp = 320, 180, 12, 2
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], fov, W / H, 1.0, 10000.0)
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
