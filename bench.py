@@ -155,6 +155,27 @@ def valu_issue(pmc, avg_launch_s, device):
             "frac": round(achieved / peak, 4), "lane_utilisation": round(pmc.get("derived", {}).get("valu_lane_utilisation", 0.0), 3)}
 
 
+class _StdoutToStderr:
+    """Points file descriptor 1 at stderr (C-level prints included) between __enter__ and __exit__."""
+
+    def __init__(self):
+        self.saved = None
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            sys.stdout.flush()
+            os.dup2(self.saved, 1)
+            os.close(self.saved)
+            self.saved = None
+        return False
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,12 +191,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # RCCL prints its version banner on stdout when a communicator is created; the contract is ONE JSON line
+    # on stdout, so descriptor 1 points at stderr until the warm-up (communicator creation included) is done
+    quiet = _StdoutToStderr()
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     use_comm = world > 1 or args.force_comm
     if use_comm:
         import torch
         import torch.distributed as tdist
+        quiet.__enter__()
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = tdist
@@ -219,6 +244,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier_sync()
+    quiet.__exit__()
     kernel_ms = 0.0
     launches = 0
     t0 = time.perf_counter()
