@@ -8,8 +8,10 @@ and (N > 1) the RCCL sum-reduce of the per-rank float4 accumulators into rank 0.
 device before timing starts (scene rows uploaded by sail_set_scene; the per-sample camera schedule is
 generated on the host and uploaded inside the step, ~64 KB, as the reference uploads uniforms per frame).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
-(one process per GPU, RCCL). Rank 0 prints one JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 either under torch.distributed.run (one
+process per GPU, WORLD_SIZE = N, RCCL communicator per process) or as one process driving N GPUs through one
+multi-device context (sail_create_multi: ncclCommInitAll + grouped reduce). Any other combination of --gpus and
+WORLD_SIZE exits non-zero. Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -191,6 +193,13 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.gpus < 1 or (world > 1 and args.gpus != world):
+        sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE {world} (one process per GPU under "
+                 "torch.distributed.run, or --gpus N in one process)")
+    # one process, N GPUs: the library's multi-device context splits the frame (no torch.distributed)
+    multi = world == 1 and args.gpus > 1
+    if multi and capi.device_count() < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but only {capi.device_count()} HIP devices are visible")
     # RCCL prints its version banner on stdout when a communicator is created; the contract is ONE JSON line
     # on stdout, so descriptor 1 points at stderr until the warm-up (communicator creation included) is done
     quiet = _StdoutToStderr()
@@ -214,12 +223,14 @@ def main():
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
 
-    ctx = capi.Context(W, H, device=local_rank)
+    ctx = capi.Context(W, H, devices=list(range(args.gpus))) if multi else capi.Context(W, H, device=local_rank)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
     part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
     flt = sc.get("filter") if cfg.get("filter") else None
     fweights = np.array(flt["weights64"], dtype=np.float32) if flt else None
+    if multi:
+        ctx.set_partition(0, 1, part)
     if use_comm:
         ctx.set_partition(rank, world, part)
         uid = [capi.comm_unique_id() if rank == 0 else None]
@@ -229,7 +240,7 @@ def main():
     def step():
         ctx.reset()
         ctx.render_schedule(inv, seeds, sc["eye"], B)
-        if use_comm:
+        if use_comm or multi:
             ctx.reduce(0)
         if flt and rank == 0:  # reconstruction filter of the reduced frame (window.glsl, gaussian r = 2)
             ctx.filter(capi.FILTER_WINDOW, fweights, flt["radius"][0], flt["radius"][1], 2.2)
@@ -264,14 +275,15 @@ def main():
 
     total_segments = W * H * spp * B * args.steps  # nominal; closed scene: every path runs all bounces
     value = total_segments / elapsed / 1e6
+    ngpu = args.gpus if multi else world
     if rank == 0:
         avg_launch_s = (kernel_ms / max(launches, 1)) / 1e3
         # this rank's pixels per launch (rank 0 at N = 1: the full frame)
-        tiles_px = W * H if (world == 1 or part == capi.PART_SAMPLES) else None
+        tiles_px = W * H if (ngpu == 1 or part == capi.PART_SAMPLES) else None
         if tiles_px is None:
             tx, ty = (W + 63) // 64, (H + 63) // 64
             tiles_px = 0
-            for t in range(0, tx * ty, world):
+            for t in range(0, tx * ty, ngpu):
                 tiles_px += min(64, W - (t % tx) * 64) * min(64, H - (t // tx) * 64)
         segs_per_launch = tiles_px * args.launch_spp * B
         ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
@@ -283,7 +295,7 @@ def main():
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": ngpu,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -294,7 +306,8 @@ def main():
             "data": f"synthetic: frozen {cfg['desc']} scene rows (SURVEY §8(d), JS API == reference serializer), "
                     "deterministic sample schedule",
             "config": {"workload": cfg["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
-                       "launch_spp": args.launch_spp, "partition": f"tiles64x{world}", "segments_per_step": W * H * spp * B},
+                       "launch_spp": args.launch_spp, "partition": f"tiles64x{ngpu}",
+                       "processes": "one per GPU" if world > 1 else ("one (multi-device context)" if multi else "one"), "segments_per_step": W * H * spp * B},
             "roofline": {
                 "bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -314,8 +327,8 @@ def main():
             rec["filter"] = {"kind": flt["name"], "kernel": "sail_filter_kernel", "avg_ms": round(fms, 4),
                              "bound": "hbm", "bytes_per_pass": fbytes, "achieved": round(fbytes / (fms * 1e-3) / 1e9, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fbytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-            rec["config"]["partition"] = f"{cfg.get('partition', 'tiles')}x{world}"
-        if not args.no_cpu_baseline and world == 1:
+            rec["config"]["partition"] = f"{cfg.get('partition', 'tiles')}x{ngpu}"
+        if not args.no_cpu_baseline and ngpu == 1:
             # the north star's JS/Node software shader; the C++ restatement is timed beside it for reference
             cpp = cpu_baseline(sc, masks, mvp, W, H, B, budget_s=5.0)
             js = cpu_baseline_js(sc, masks, mvp, W, H, B)

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SAIL_ABI_VERSION 1
+#define SAIL_ABI_VERSION 2
 
 enum sail_status {
   SAIL_OK = 0,
@@ -73,6 +73,15 @@ typedef struct sail_ctx sail_ctx;
 /* new Sail.Renderer(canvas) (src/core/renderer.js:9-39): one device, a W x H float accumulator.
  * device < 0 uses the current device. */
 int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flags);
+/* new Sail.Renderer({devices: N}): ONE context over n_devices GPUs of this process (devices = NULL: 0..n-1).
+ * The reference renders on one WebGL context (src/core/renderer.js:9-39, tracer.js:92-101); here the frame's
+ * 64x64 tiles (or, after sail_set_partition(ctx, 0, 1, SAIL_PART_SAMPLES), its samples) are dealt across the
+ * devices, each renders its share on its own stream, and readback / read_accum / filter first sum the devices'
+ * accumulators into device 0 with one grouped RCCL reduce over a ncclCommInitAll communicator (progressive:
+ * the sum is recomputed from the cumulative accumulators whenever something was rendered since). Every other
+ * entry point fans out. Devices must be all distinct (RCCL over xGMI) or all the same one (the partition runs on
+ * one GPU and a kernel sums it: the emulation the parity tests use). sail_comm_init is refused on it. */
+int sail_create_multi(sail_ctx** out, int width, int height, const int* devices, int n_devices, uint32_t flags);
 void sail_destroy(sail_ctx* ctx);
 const char* sail_last_error(const sail_ctx* ctx); /* ctx may be NULL: last creation error */
 int sail_device_count(int* count);
@@ -90,6 +99,15 @@ int sail_update_objects(sail_ctx* ctx, const float* objects, int n);
 int sail_set_accum_mode(sail_ctx* ctx, int mode);        /* resets accumulation */
 int sail_set_partition(sail_ctx* ctx, int rank, int world, int mode);
 int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch (default 32) */
+/* Test / study switches (no reference counterpart; none changes a result, which the parity suite checks).
+ * The product's defaults are the values in brackets. */
+enum sail_debug_option {
+  SAIL_DEBUG_CULL_MIN_PRIMS = 1, /* scenes with >= value primitives use the padded-box pre-cull kernel [8] */
+  SAIL_DEBUG_FORCE_GENERIC = 2,  /* 1: always launch the all-plugin kernel [0] */
+  SAIL_DEBUG_CULL_FMA = 3,       /* 0: the plain pre-cull slab form instead of the fused one [1] */
+  SAIL_DEBUG_SAMPLE_GROUPS = 4   /* > 0: fixed sample-group count per 16x16 block [0 = sized by occupancy] */
+};
+int sail_set_debug(sail_ctx* ctx, int option, int value);
 
 /* Tracer.render(mvp, eye, k) (src/core/tracer.js:92-101) = one progressive sample with the caller's
  * jittered inverse matrix (16 f32, column-major as uniformMatrix4fv uploads it, webgl.js:103) and seed. */
@@ -130,9 +148,16 @@ int sail_schedule(const double mvp_rowmajor[16], int width, int height, int k0, 
 
 /* ---- multi-GPU (one process per GPU): image tiles / sample split + RCCL sum-reduce of the accumulators ---- */
 int sail_comm_unique_id(char id[128]);
+/* a second call replaces the communicator */
 int sail_comm_init(sail_ctx* ctx, const char id[128], int nranks, int rank);
-int sail_reduce(sail_ctx* ctx, int root);                /* in-place sum of the float4 accumulators into root */
-int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes); /* for an external collective */
+/* Sum of every rank's float4 accumulator (and, with SAIL_FLAG_AOV on a tile partition, of the AOV maps) into a
+ * separate frame on `root`; collective: every rank calls it, all created with the same flags. The ranks'
+ * accumulators are left as they are, so render -> reduce -> render -> reduce is progressive: each reduce sums
+ * the cumulative accumulators afresh. On root, readback / read_accum / filter show that frame until the next
+ * sail_render* or sail_reset (then this rank's own accumulator again). Asynchronous RCCL errors are reported
+ * here and by sail_sync (ncclCommGetAsyncError). On a multi-device context it reduces into device 0 (root 0). */
+int sail_reduce(sail_ctx* ctx, int root);
+int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes); /* this rank's (device 0's) accumulator */
 /* the 64x64 tiles rank `rank` of `world` owns in a W x H frame (tile t -> rank t % world), as
  * (x0, y0, w, h) quadruples; returns the tile count (or a negative error); out may be NULL to count */
 int sail_partition_tiles(int width, int height, int rank, int world, int* out_xywh, int capacity);

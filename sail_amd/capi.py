@@ -22,10 +22,14 @@ ACCUM_SUM, ACCUM_MIX, ACCUM_COMPAT8 = 0, 1, 2
 PART_TILES, PART_SAMPLES = 0, 1
 FILTER_COLOR, FILTER_GAMMA, FILTER_TONEMAPPING, FILTER_WINDOW = 0, 1, 2, 3
 FILTER_WAVELET, FILTER_NORMAL, FILTER_POSITION = 4, 5, 6  # need FLAG_AOV
+# sail_set_debug options (test / study switches; none changes a result)
+DEBUG_CULL_MIN_PRIMS, DEBUG_FORCE_GENERIC, DEBUG_CULL_FMA, DEBUG_SAMPLE_GROUPS = 1, 2, 3, 4
+# applied to every Context at creation (tests set entries with monkeypatch.setitem)
+DEBUG_DEFAULTS: dict = {}
 
 # exported symbols (kept in sync with include/sail_hip.h; tests/test_capi_symbols.py checks both ways)
 EXPORTS = (
-    "sail_create", "sail_destroy", "sail_last_error", "sail_device_count", "sail_device_info", "sail_set_scene",
+    "sail_create", "sail_create_multi", "sail_set_debug", "sail_destroy", "sail_last_error", "sail_device_count", "sail_device_info", "sail_set_scene",
     "sail_update_objects", "sail_set_accum_mode", "sail_set_partition", "sail_set_launch_samples",
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
@@ -85,6 +89,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     vp = ctypes.c_void_p
     sig = {
         "sail_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]),
+        "sail_create_multi": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.c_int, ctypes.c_uint32]),
+        "sail_set_debug": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
         "sail_destroy": (None, [vp]),
         "sail_last_error": (ctypes.c_char_p, [vp]),
         "sail_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
@@ -218,16 +225,30 @@ def comm_unique_id() -> bytes:
 
 
 class Context:
-    """One device context: the MI355X counterpart of Sail's Renderer/Tracer GPU state."""
+    """A device context: the MI355X counterpart of Sail's Renderer/Tracer GPU state. With `devices` (a list of
+    device ordinals) it is one multi-device context (sail_create_multi): the frame is split across them and
+    reduced into device 0 on readback."""
 
-    def __init__(self, width: int, height: int, device: int = -1, flags: int = 0):
+    def __init__(self, width: int, height: int, device: int = -1, flags: int = 0, devices: Optional[Sequence[int]] = None,
+                 debug: Optional[dict] = None):
         self.lib = load()
         self.W, self.H = int(width), int(height)
         h = ctypes.c_void_p()
-        rc = self.lib.sail_create(ctypes.byref(h), self.W, self.H, device, flags)
+        if devices is not None:
+            dv = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            rc = self.lib.sail_create_multi(ctypes.byref(h), self.W, self.H, dv, len(devices), flags)
+            what = "sail_create_multi"
+        else:
+            rc = self.lib.sail_create(ctypes.byref(h), self.W, self.H, device, flags)
+            what = "sail_create"
         if rc:
-            raise SailError(f"sail_create: {rc}: {self.lib.sail_last_error(None).decode()}")
+            raise SailError(f"{what}: {rc}: {self.lib.sail_last_error(None).decode()}")
         self.h = h
+        for opt, val in {**DEBUG_DEFAULTS, **(debug or {})}.items():
+            self.set_debug(opt, val)
+
+    def set_debug(self, option: int, value: int):
+        self._check(self.lib.sail_set_debug(self.h, int(option), int(value)), "sail_set_debug")
 
     def _check(self, rc: int, what: str):
         if rc:

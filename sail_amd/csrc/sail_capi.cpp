@@ -18,6 +18,8 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
+hipError_t sail_launch_sum(const SailSumArgs& A, hipStream_t s);
+hipError_t sail_launch_negzero_unowned(float4* a, float4* b, int W, int H, int rank, int world, hipStream_t s);
 hipError_t sail_launch_pick(const SailPrim* prims, int n, const float* rays, int count, int32_t* index, float* t,
                             hipStream_t s);
 
@@ -34,6 +36,10 @@ struct Rccl {
   int (*commInitRank)(nccl_comm_t*, int, nccl_uid_t, int) = nullptr;
   int (*reduce)(const void*, void*, size_t, int, int, int, nccl_comm_t, hipStream_t) = nullptr;
   int (*commDestroy)(nccl_comm_t) = nullptr;
+  int (*commInitAll)(nccl_comm_t*, int, const int*) = nullptr;   // single-process multi-device communicator
+  int (*groupStart)() = nullptr;
+  int (*groupEnd)() = nullptr;
+  int (*commGetAsyncError)(nccl_comm_t, int*) = nullptr;
   const char* (*errStr)(int) = nullptr;
   bool load() {
     if (tried) return ok;
@@ -47,7 +53,12 @@ struct Rccl {
     reduce = (int (*)(const void*, void*, size_t, int, int, int, nccl_comm_t, hipStream_t))dlsym(h, "ncclReduce");
     commDestroy = (int (*)(nccl_comm_t))dlsym(h, "ncclCommDestroy");
     errStr = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
-    ok = getUniqueId && commInitRank && reduce && commDestroy;
+    commInitAll = (int (*)(nccl_comm_t*, int, const int*))dlsym(h, "ncclCommInitAll");
+    groupStart = (int (*)())dlsym(h, "ncclGroupStart");
+    groupEnd = (int (*)())dlsym(h, "ncclGroupEnd");
+    commGetAsyncError = (int (*)(nccl_comm_t, int*))dlsym(h, "ncclCommGetAsyncError");
+    ok = getUniqueId && commInitRank && reduce && commDestroy && commInitAll && groupStart && groupEnd &&
+         commGetAsyncError;
     return ok;
   }
 };
@@ -140,6 +151,20 @@ struct sail_ctx {
   uint32_t launches = 0;
   nccl_comm_t comm = nullptr;
   int commRanks = 0, commRank = 0;
+  // Reduced frame (root of sail_reduce / device 0 of a multi-device context): the sum of every rank's
+  // cumulative accumulator, recomputed from scratch by each reduce, so render -> reduce -> render -> reduce
+  // never counts a sample twice. While `reduced` is set, readback / read_accum / filter show this frame.
+  float4* frame = nullptr;
+  float4* frameN = nullptr;  // reduced AOVs (SAIL_FLAG_AOV)
+  float4* frameP = nullptr;
+  bool reduced = false;
+  // Multi-device context (sail_create_multi): one sub-context per device, each rendering its share of the
+  // partition on its own stream; `dirty` = rendered since the last reduce. Devices are all distinct (grouped
+  // RCCL reduce over a ncclCommInitAll communicator) or all the same one (`groupLocal`: summed by a kernel).
+  std::vector<sail_ctx*> subs;
+  std::vector<nccl_comm_t> groupComms;
+  bool groupLocal = false;
+  bool dirty = false;
   float eyeCache[3] = {0.0f, 0.0f, 0.0f};
   std::string err;
 };
@@ -155,7 +180,12 @@ int fail(sail_ctx* c, int code, const char* fmt, ...) {
   if (c) c->err = buf; else g_create_error = buf;
   return code;
 }
-#define HIPCHK(ctx, call)                                                                          \
+// a multi-device context's call failed in one of its sub-contexts: carry that context's message up
+int relay(sail_ctx* c, int rc, const sail_ctx* sub) {
+  if (rc != SAIL_OK && sub && c != sub) c->err = sub->err;
+  return rc;
+}
+#define HIPCHK(ctx, call)                                                                       \
   do {                                                                                             \
     hipError_t e_ = (call);                                                                        \
     if (e_ != hipSuccess) return fail((ctx), SAIL_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
@@ -226,10 +256,13 @@ void cornerDirs(const float* M, const float* eye, float out[4][3]) {
 }
 
 int resetAccum(sail_ctx* c) {
+  c->reduced = false;
   const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
   HIPCHK(c, hipMemsetAsync(c->accum, 0, bytes, c->stream));
   if (c->aovN) HIPCHK(c, hipMemsetAsync(c->aovN, 0, bytes, c->stream));
   if (c->aovP) HIPCHK(c, hipMemsetAsync(c->aovP, 0, bytes, c->stream));
+  if ((c->aovN || c->aovP) && c->partMode == SAIL_PART_TILES && c->world > 1)
+    HIPCHK(c, sail_launch_negzero_unowned(c->aovN, c->aovP, c->W, c->H, c->rank, c->world, c->stream));
   if (c->segCounter) HIPCHK(c, hipMemsetAsync(c->segCounter, 0, SAIL_SEG_SLOTS * sizeof(unsigned long long), c->stream));
   int rc = collectEvents(c);
   if (rc) return rc;
@@ -602,6 +635,86 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   return SAIL_OK;
 }
 
+// ---- reduced frame (sail_reduce, multi-device contexts) -----------------------------------------------------------
+int ensureFrame(sail_ctx* c) {
+  const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  float4** bufs[3] = {&c->frame, c->aovN ? &c->frameN : nullptr, c->aovP ? &c->frameP : nullptr};
+  for (float4** b : bufs) {
+    if (!b || *b) continue;
+    if (hipMalloc(b, bytes) != hipSuccess) { *b = nullptr; return fail(c, SAIL_E_OOM, "reduced frame"); }
+  }
+  return SAIL_OK;
+}
+// the buffers readback / filter show: the last reduced frame while it is current, else this rank's own
+const float4* shownAccum(const sail_ctx* c) { return c->reduced ? c->frame : c->accum; }
+const float4* shownAovN(const sail_ctx* c) { return c->reduced && c->frameN ? c->frameN : c->aovN; }
+const float4* shownAovP(const sail_ctx* c) { return c->reduced && c->frameP ? c->frameP : c->aovP; }
+
+// asynchronous RCCL errors (ncclCommGetAsyncError): a failed collective surfaces here, not at enqueue time
+int commCheck(sail_ctx* c, nccl_comm_t comm) {
+  if (!comm || !g_rccl.commGetAsyncError) return SAIL_OK;
+  int ae = 0;
+  const int r = g_rccl.commGetAsyncError(comm, &ae);
+  constexpr int kNcclInProgress = 7;  // non-blocking communicators only; this library creates blocking ones
+  if (r != 0 || (ae != 0 && ae != kNcclInProgress)) {
+    const int code = r ? r : ae;
+    return fail(c, SAIL_E_RCCL, "RCCL communicator error %d: %s", code, g_rccl.errStr ? g_rccl.errStr(code) : "?");
+  }
+  return SAIL_OK;
+}
+int groupCommCheck(sail_ctx* g) {
+  for (nccl_comm_t cm : g->groupComms) if (int rc = commCheck(g, cm)) return rc;
+  return SAIL_OK;
+}
+
+// Multi-device context: device 0's frame = the sum of every device's cumulative accumulator (and, for tile
+// partitions, of the AOV maps: -0 outside each device's tiles, so the sum is exact). Recomputed from scratch
+// whenever something was rendered since the last one, so progressive frames never count a sample twice.
+// Sample partitions show device 0's AOVs (each device's maps hold its own last sample).
+int groupReduce(sail_ctx* g) {
+  const int nd = (int)g->subs.size();
+  sail_ctx* r = g->subs[0];
+  if (nd == 1 || !g->dirty) return SAIL_OK;
+  HIPCHK(g, hipSetDevice(r->device));
+  if (int rc = ensureFrame(r)) return relay(g, rc, r);
+  const bool tiles = g->partMode == SAIL_PART_TILES;
+  const size_t np = (size_t)g->W * g->H, bytes = np * sizeof(float4);
+  if (g->groupLocal) {  // every "device" is the same GPU: wait for the others' streams, sum in rank order
+    for (sail_ctx* s : g->subs) HIPCHK(g, hipStreamSynchronize(s->stream));
+    auto sum = [&](float4* dst, float4* sail_ctx::*src) -> hipError_t {
+      SailSumArgs A;
+      memset(&A, 0, sizeof A);
+      A.dst = dst; A.n = (long long)np; A.nsrc = nd;
+      for (int i = 0; i < nd; i++) A.src[i] = g->subs[i]->*src;
+      return sail_launch_sum(A, r->stream);
+    };
+    HIPCHK(g, sum(r->frame, &sail_ctx::accum));
+    if (r->aovN) HIPCHK(g, tiles ? sum(r->frameN, &sail_ctx::aovN) : hipMemcpyAsync(r->frameN, r->aovN, bytes, hipMemcpyDeviceToDevice, r->stream));
+    if (r->aovP) HIPCHK(g, tiles ? sum(r->frameP, &sail_ctx::aovP) : hipMemcpyAsync(r->frameP, r->aovP, bytes, hipMemcpyDeviceToDevice, r->stream));
+    HIPCHK(g, hipStreamSynchronize(r->stream));  // the other devices' next renders may overwrite their inputs
+  } else {  // one grouped RCCL reduce into device 0 over the ncclCommInitAll communicator
+    int e = g_rccl.groupStart();
+    for (int i = 0; i < nd && e == 0; i++) {
+      sail_ctx* s = g->subs[i];
+      if (hipSetDevice(s->device) != hipSuccess) { e = -1; break; }
+      e = g_rccl.reduce(s->accum, i == 0 ? r->frame : s->accum, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
+      if (e == 0 && tiles && s->aovN)
+        e = g_rccl.reduce(s->aovN, i == 0 ? r->frameN : s->aovN, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
+      if (e == 0 && tiles && s->aovP)
+        e = g_rccl.reduce(s->aovP, i == 0 ? r->frameP : s->aovP, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
+    }
+    const int e2 = g_rccl.groupEnd();
+    if (e || e2) return fail(g, SAIL_E_RCCL, "grouped ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(e ? e : e2) : "?");
+    HIPCHK(g, hipSetDevice(r->device));
+    if (!tiles && r->aovN) HIPCHK(g, hipMemcpyAsync(r->frameN, r->aovN, bytes, hipMemcpyDeviceToDevice, r->stream));
+    if (!tiles && r->aovP) HIPCHK(g, hipMemcpyAsync(r->frameP, r->aovP, bytes, hipMemcpyDeviceToDevice, r->stream));
+    if (int rc = groupCommCheck(g)) return rc;
+  }
+  r->reduced = true;
+  g->dirty = false;
+  return SAIL_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -610,12 +723,14 @@ int sail_abi_version(void) { return SAIL_ABI_VERSION; }
 
 int sail_filter_ms(sail_ctx* c, double* ms) {
   if (!c || !ms) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return sail_filter_ms(c->subs[0], ms);
   *ms = c->lastFilterMs;
   return SAIL_OK;
 }
 
 int sail_kernel_name(sail_ctx* c, char* name, int len) {
   if (!c || !name || len <= 0) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return relay(c, sail_kernel_name(c->subs[0], name, len), c->subs[0]);
   if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_kernel_name: no scene");
   const int set = kernelSetFor(c);
   const char* k = set == SAIL_KSET_CORNELL ? "sail_trace_kernel_cornell"
@@ -656,10 +771,6 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
   if (device >= ndev) return fail(nullptr, SAIL_E_INVALID, "device %d out of range (%d devices)", device, ndev);
   sail_ctx* c = new sail_ctx();
   c->device = device; c->W = width; c->H = height; c->flags = flags;
-  if (const char* e = getenv("SAIL_CULL_MIN_PRIMS")) c->cullMinPrims = atoi(e);  // tests force the pre-cull on/off
-  if (const char* e = getenv("SAIL_FORCE_GENERIC")) c->forceGeneric = atoi(e);
-  if (const char* e = getenv("SAIL_CULL_FMA")) c->cullFma = atoi(e);
-  if (const char* e = getenv("SAIL_SAMPLE_GROUPS")) c->forceGroups = atoi(e);
   auto bail = [&](int code, const char* what) {
     g_create_error = std::string("sail_create: ") + what;
     sail_destroy(c);
@@ -687,16 +798,79 @@ int sail_create(sail_ctx** out, int width, int height, int device, uint32_t flag
 
 void sail_destroy(sail_ctx* c) {
   if (!c) return;
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (s) { (void)hipSetDevice(s->device); (void)hipStreamSynchronize(s->stream); }
+    for (nccl_comm_t cm : c->groupComms) if (cm && g_rccl.commDestroy) g_rccl.commDestroy(cm);
+    for (sail_ctx* s : c->subs) sail_destroy(s);
+    delete c;
+    return;
+  }
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
   for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->evPool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->accum, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
+  void* bufs[] = {c->accum, c->frame, c->frameN, c->frameP, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (c->samplesPinned) (void)hipHostFree(c->samplesPinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+int sail_create_multi(sail_ctx** out, int width, int height, const int* devices, int n_devices, uint32_t flags) {
+  if (!out || n_devices < 1 || n_devices > 64)
+    return fail(nullptr, SAIL_E_INVALID, "sail_create_multi: bad arguments (%d devices)", n_devices);
+  *out = nullptr;
+  std::vector<int> dev((size_t)n_devices);
+  for (int i = 0; i < n_devices; i++) dev[i] = devices ? devices[i] : i;
+  bool allSame = true, allDistinct = true;
+  for (int i = 0; i < n_devices; i++)
+    for (int j = 0; j < n_devices; j++) {
+      if (dev[i] != dev[j]) allSame = false;
+      if (i != j && dev[i] == dev[j]) allDistinct = false;
+    }
+  if (!allSame && !allDistinct)
+    return fail(nullptr, SAIL_E_INVALID, "sail_create_multi: devices must be all distinct or all the same one");
+  sail_ctx* g = new sail_ctx();
+  g->W = width; g->H = height; g->flags = flags; g->device = dev[0];
+  g->world = n_devices;
+  g->groupLocal = n_devices > 1 && allSame;
+  for (int i = 0; i < n_devices; i++) {
+    sail_ctx* s = nullptr;
+    int rc = sail_create(&s, width, height, dev[i], flags);
+    if (rc == SAIL_OK) g->subs.push_back(s);
+    if (rc == SAIL_OK) rc = sail_set_partition(s, i, n_devices, SAIL_PART_TILES);
+    if (rc != SAIL_OK) {
+      const std::string msg = s ? s->err : g_create_error;
+      sail_destroy(g);
+      return fail(nullptr, rc, "sail_create_multi: device %d: %s", dev[i], msg.c_str());
+    }
+  }
+  if (n_devices > 1 && allDistinct) {
+    if (!g_rccl.load()) { sail_destroy(g); return fail(nullptr, SAIL_E_RCCL, "sail_create_multi: librccl not loadable"); }
+    g->groupComms.assign((size_t)n_devices, nullptr);
+    const int r = g_rccl.commInitAll(g->groupComms.data(), n_devices, dev.data());
+    if (r) {
+      g->groupComms.clear();
+      sail_destroy(g);
+      return fail(nullptr, SAIL_E_RCCL, "ncclCommInitAll: %s", g_rccl.errStr ? g_rccl.errStr(r) : "?");
+    }
+  }
+  *out = g;
+  return SAIL_OK;
+}
+
+int sail_set_debug(sail_ctx* c, int option, int value) {
+  if (!c) return SAIL_E_INVALID;
+  for (sail_ctx* s : c->subs) if (int rc = sail_set_debug(s, option, value)) return relay(c, rc, s);
+  switch (option) {
+    case SAIL_DEBUG_CULL_MIN_PRIMS: c->cullMinPrims = value; break;
+    case SAIL_DEBUG_FORCE_GENERIC: c->forceGeneric = value; break;
+    case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
+    case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
+    default: return fail(c, SAIL_E_INVALID, "sail_set_debug: unknown option %d", option);
+  }
+  return SAIL_OK;
 }
 
 // The primitive buffer holds the decoded rows followed by the candidate sweep's per-type masks: for each chunk
@@ -721,6 +895,12 @@ static int uploadPrims(sail_ctx* c, const std::vector<SailPrim>& prims) {
 int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texparams, int tn, const float* lights,
                    int ln, const sail_plugins* plugins) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs)
+      if (int rc = sail_set_scene(s, objects, n, texparams, tn, lights, ln, plugins)) return relay(c, rc, s);
+    c->haveScene = true; c->n = n; c->tn = tn; c->ln = ln; c->dirty = false;
+    return SAIL_OK;
+  }
   if (n < 0 || tn < 0 || ln < 0 || (n > 0 && !objects) || (tn > 0 && !texparams) || (ln > 0 && !lights) || !plugins)
     return fail(c, SAIL_E_INVALID, "sail_set_scene: bad arguments (n=%d tn=%d ln=%d)", n, tn, ln);
   if (n > 0 && tn < 1) return fail(c, SAIL_E_INVALID, "sail_set_scene: objects need texParams rows");
@@ -762,6 +942,11 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
 }
 
 int sail_update_objects(sail_ctx* c, const float* objects, int n) {
+  if (c && !c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (int rc = sail_update_objects(s, objects, n)) return relay(c, rc, s);
+    c->dirty = false;
+    return SAIL_OK;
+  }
   if (!c || !c->haveScene) return c ? fail(c, SAIL_E_STATE, "sail_update_objects before sail_set_scene") : SAIL_E_INVALID;
   if (n != c->n || !objects) return fail(c, SAIL_E_INVALID, "sail_update_objects: n must stay %d", c->n);
   HIPCHK(c, hipSetDevice(c->device));
@@ -779,6 +964,11 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
 int sail_set_accum_mode(sail_ctx* c, int mode) {
   if (!c) return SAIL_E_INVALID;
   if (mode < SAIL_ACCUM_SUM || mode > SAIL_ACCUM_COMPAT8) return fail(c, SAIL_E_INVALID, "accum mode %d", mode);
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (int rc = sail_set_accum_mode(s, mode)) return relay(c, rc, s);
+    c->accumMode = mode; c->dirty = false;
+    return SAIL_OK;
+  }
   if (mode != SAIL_ACCUM_SUM && c->partMode == SAIL_PART_SAMPLES && c->world > 1)
     return fail(c, SAIL_E_INVALID, "running-mean accumulation cannot be split by samples");
   HIPCHK(c, hipSetDevice(c->device));
@@ -788,6 +978,14 @@ int sail_set_accum_mode(sail_ctx* c, int mode) {
 
 int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {  // the devices of one context split the frame among themselves: only the mode is chosen
+    if (rank != 0 || world != 1 || (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
+      return fail(c, SAIL_E_INVALID, "multi-device context: partition must be (0, 1, mode), got (%d, %d, %d)", rank, world, mode);
+    const int nd = (int)c->subs.size();
+    for (int i = 0; i < nd; i++) if (int rc = sail_set_partition(c->subs[i], i, nd, mode)) return relay(c, rc, c->subs[i]);
+    c->partMode = mode; c->dirty = false;
+    return SAIL_OK;
+  }
   if (world < 1 || rank < 0 || rank >= world || (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
     return fail(c, SAIL_E_INVALID, "partition rank=%d world=%d mode=%d", rank, world, mode);
   if (mode == SAIL_PART_SAMPLES && world > 1 && c->accumMode != SAIL_ACCUM_SUM)
@@ -800,12 +998,19 @@ int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
 int sail_set_launch_samples(sail_ctx* c, int spp) {
   if (!c) return SAIL_E_INVALID;
   if (spp < 1 || spp > 1 << 20) return fail(c, SAIL_E_INVALID, "launch samples %d", spp);
+  for (sail_ctx* s : c->subs) if (int rc = sail_set_launch_samples(s, spp)) return relay(c, rc, s);
   c->launchSpp = spp;
   return SAIL_OK;
 }
 
 int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, const float eye[3], int spp, int maxBounces) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {  // every device queues its share on its own stream; the host does not wait
+    for (sail_ctx* s : c->subs)
+      if (int rc = sail_render_schedule(s, inv, seeds, eye, spp, maxBounces)) return relay(c, rc, s);
+    c->dirty = true;
+    return SAIL_OK;
+  }
   if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_render before sail_set_scene");
   if (spp < 0 || (spp > 0 && (!inv || !seeds)) || !eye || maxBounces < 0 || maxBounces > 1024)
     return fail(c, SAIL_E_INVALID, "sail_render_schedule: bad arguments (spp=%d bounces=%d)", spp, maxBounces);
@@ -824,6 +1029,7 @@ int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, cons
   }
   const int rc = launchTrace(c, c->hostSamples.data(), (int)c->hostSamples.size(), maxBounces);
   if (rc) return rc;
+  c->reduced = false;  // the frame of the last sail_reduce is stale now: reduce again to refresh it
   c->samplesThisRank += c->hostSamples.size();
   c->k += (uint64_t)spp;
   return SAIL_OK;
@@ -835,32 +1041,50 @@ int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed
 
 int sail_reset(sail_ctx* c) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (int rc = sail_reset(s)) return relay(c, rc, s);
+    c->dirty = false;
+    return SAIL_OK;
+  }
   HIPCHK(c, hipSetDevice(c->device));
   return resetAccum(c);
 }
 
 int sail_sync(sail_ctx* c) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (int rc = sail_sync(s)) return relay(c, rc, s);
+    return groupCommCheck(c);
+  }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (int rc = commCheck(c, c->comm)) return rc;
   return collectEvents(c);
 }
 
 int sail_read_accum(sail_ctx* c, float* rgba) {
   if (!c || !rgba) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    if (int rc = groupReduce(c)) return rc;
+    return relay(c, sail_read_accum(c->subs[0], rgba), c->subs[0]);
+  }
   int rc = sail_sync(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemcpy(rgba, c->accum, (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(rgba, shownAccum(c), (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
   return SAIL_OK;
 }
 
 int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    if (int rc = groupReduce(c)) return rc;
+    return relay(c, sail_readback(c->subs[0], rgba, normal, position), c->subs[0]);
+  }
   int rc = sail_sync(c);
   if (rc) return rc;
   const size_t np = (size_t)c->W * c->H, bytes = np * sizeof(float4);
   if (rgba) {
-    HIPCHK(c, hipMemcpy(rgba, c->accum, bytes, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(rgba, shownAccum(c), bytes, hipMemcpyDeviceToHost));
     if (c->accumMode == SAIL_ACCUM_SUM) {
       for (size_t i = 0; i < np; i++) {
         const float cnt = rgba[4 * i + 3];
@@ -871,17 +1095,21 @@ int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
   }
   if (normal) {
     if (!c->aovN) return fail(c, SAIL_E_STATE, "AOVs not enabled (SAIL_FLAG_AOV)");
-    HIPCHK(c, hipMemcpy(normal, c->aovN, bytes, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(normal, shownAovN(c), bytes, hipMemcpyDeviceToHost));
   }
   if (position) {
     if (!c->aovP) return fail(c, SAIL_E_STATE, "AOVs not enabled (SAIL_FLAG_AOV)");
-    HIPCHK(c, hipMemcpy(position, c->aovP, bytes, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(position, shownAovP(c), bytes, hipMemcpyDeviceToHost));
   }
   return SAIL_OK;
 }
 
 int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float ry, float gammaC, float* out, uint8_t* out8) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {  // the display pass runs on device 0 over the reduced frame
+    if (int rc = groupReduce(c)) return rc;
+    return relay(c, sail_filter(c->subs[0], kind, weights16, rx, ry, gammaC, out, out8), c->subs[0]);
+  }
   if (kind < SAIL_FILTER_COLOR || kind > SAIL_FILTER_POSITION || (kind == SAIL_FILTER_WINDOW && !weights16))
     return fail(c, SAIL_E_INVALID, "sail_filter: kind %d", kind);
   if (kind >= SAIL_FILTER_WAVELET && !c->aovN)
@@ -902,15 +1130,8 @@ int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float r
   uint8_t* dOut8 = out8 ? c->filterOut8 : nullptr;
   SailFilterArgs A;
   memset(&A, 0, sizeof A);
-  A.accum = c->accum; A.aovN = c->aovN; A.aovP = c->aovP; A.out = dOut; A.out8 = dOut8; A.W = c->W; A.H = c->H; A.kind = kind; A.accumMode = c->accumMode;
-  // a SUM accumulator holds the same count in every pixel of a frame (all pixels get every sample)
-  float cnt = 1.0f;
-  if (c->accumMode == SAIL_ACCUM_SUM) {
-    float4 px0;
-    HIPCHK(c, hipMemcpy(&px0, c->accum, sizeof px0, hipMemcpyDeviceToHost));
-    cnt = px0.w > 0.0f ? px0.w : 1.0f;
-  }
-  A.count = cnt; A.invCount = 1.0f / cnt;
+  A.accum = shownAccum(c); A.aovN = shownAovN(c); A.aovP = shownAovP(c);
+  A.out = dOut; A.out8 = dOut8; A.W = c->W; A.H = c->H; A.kind = kind; A.accumMode = c->accumMode;
   if (weights16) memcpy(A.weights, weights16, sizeof A.weights);
   A.rx = rx; A.ry = ry; A.gammaC = gammaC;
   // window taps reach 0.875 r pixels (offsets (j + 0.5) r / 4, j < 4) + the bilinear footprint + rounding
@@ -942,6 +1163,7 @@ int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float r
 
 int sail_pick(sail_ctx* c, const float* rays, int count, int32_t* index, float* t) {
   if (!c || count < 0 || (count > 0 && (!rays || !index || !t))) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return relay(c, sail_pick(c->subs[0], rays, count, index, t), c->subs[0]);
   if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_pick: no scene (call sail_set_scene first)");
   if (count == 0) return SAIL_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -966,6 +1188,20 @@ int sail_pick(sail_ctx* c, const float* rays, int count, int32_t* index, float* 
 
 int sail_get_stats(sail_ctx* c, sail_stats* s) {
   if (!c || !s) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {  // samples per pixel of the frame; work summed; time = the slowest device's
+    memset(s, 0, sizeof *s);
+    for (sail_ctx* d : c->subs) {
+      sail_stats q;
+      if (int rc = sail_get_stats(d, &q)) return relay(c, rc, d);
+      s->samples = c->partMode == SAIL_PART_SAMPLES ? s->samples + q.samples : q.samples;
+      s->segments += q.segments;
+      s->nominal_segments += q.nominal_segments;
+      s->kernel_ms = fmax(s->kernel_ms, q.kernel_ms);
+      s->last_launch_ms = fmax(s->last_launch_ms, q.last_launch_ms);
+      s->launches = q.launches > s->launches ? q.launches : s->launches;
+    }
+    return SAIL_OK;
+  }
   int rc = sail_sync(c);
   if (rc) return rc;
   memset(s, 0, sizeof *s);
@@ -985,6 +1221,7 @@ int sail_get_stats(sail_ctx* c, sail_stats* s) {
 
 int sail_accum_device_ptr(sail_ctx* c, void** ptr, size_t* bytes) {
   if (!c || !ptr || !bytes) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return relay(c, sail_accum_device_ptr(c->subs[0], ptr, bytes), c->subs[0]);
   *ptr = c->accum;
   *bytes = (size_t)c->W * c->H * sizeof(float4);
   return SAIL_OK;
@@ -1002,8 +1239,15 @@ int sail_comm_unique_id(char id[128]) {
 
 int sail_comm_init(sail_ctx* c, const char id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return fail(c, SAIL_E_STATE, "a multi-device context reduces over its own communicator");
   if (!g_rccl.load()) return fail(c, SAIL_E_RCCL, "librccl not loadable");
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->comm) {  // a second init replaces the communicator
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    g_rccl.commDestroy(c->comm);
+    c->comm = nullptr;
+    c->commRanks = 0; c->commRank = 0;
+  }
   nccl_uid_t u;
   memcpy(u.internal, id, 128);
   const int r = g_rccl.commInitRank(&c->comm, nranks, u, rank);
@@ -1014,11 +1258,31 @@ int sail_comm_init(sail_ctx* c, const char id[128], int nranks, int rank) {
 
 int sail_reduce(sail_ctx* c, int root) {
   if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    if (root != 0) return fail(c, SAIL_E_INVALID, "multi-device context: the frame is reduced into device 0");
+    c->dirty = true;  // reduce now even if nothing was rendered since the last one
+    return groupReduce(c);
+  }
   if (!c->comm) return fail(c, SAIL_E_STATE, "sail_reduce before sail_comm_init");
+  if (root < 0 || root >= c->commRanks) return fail(c, SAIL_E_INVALID, "sail_reduce: root %d of %d ranks", root, c->commRanks);
   HIPCHK(c, hipSetDevice(c->device));
+  const bool isRoot = c->commRank == root;
+  if (isRoot) { if (int rc = ensureFrame(c)) return rc; }
+  // out of place into root's frame: every reduce sums the ranks' cumulative accumulators afresh
   const size_t count = (size_t)c->W * c->H * 4;
-  const int r = g_rccl.reduce(c->accum, c->accum, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
-  if (r) return fail(c, SAIL_E_RCCL, "ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(r) : "?");
+  const bool tiles = c->partMode == SAIL_PART_TILES;
+  int r = g_rccl.groupStart();
+  if (r == 0) r = g_rccl.reduce(c->accum, isRoot ? c->frame : c->accum, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  if (r == 0 && tiles && c->aovN) r = g_rccl.reduce(c->aovN, isRoot ? c->frameN : c->aovN, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  if (r == 0 && tiles && c->aovP) r = g_rccl.reduce(c->aovP, isRoot ? c->frameP : c->aovP, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  const int r2 = g_rccl.groupEnd();
+  if (r || r2) return fail(c, SAIL_E_RCCL, "ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(r ? r : r2) : "?");
+  if (isRoot && !tiles) {  // a sample split shows root's own AOVs
+    if (c->aovN) HIPCHK(c, hipMemcpyAsync(c->frameN, c->aovN, count * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (c->aovP) HIPCHK(c, hipMemcpyAsync(c->frameP, c->aovP, count * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (int rc = commCheck(c, c->comm)) return rc;
+  c->reduced = isRoot;
   return SAIL_OK;
 }
 

@@ -96,10 +96,17 @@ struct SailFilterArgs {
   uint8_t* out8;
   int W, H;
   int kind;                 // 0 color, 1 gamma, 2 tonemapping, 3 window, 4 wavelet, 5 normal, 6 position
-  int accumMode;
-  float invCount;           // unused for mix modes
-  float count;
+  int accumMode;            // SUM: every texel is divided by its own count (.w)
   float weights[16];
   float rx, ry, gammaC;
   int halo;                 // window filters: LDS tile halo in pixels (0: taps read global memory)
+};
+
+// multi-device frame reduction on one GPU (sail_sum_kernel): dst = the sum of src[0..nsrc) in rank order
+#define SAIL_SUM_MAX_SRC 64
+struct SailSumArgs {
+  const float4* src[SAIL_SUM_MAX_SRC];
+  float4* dst;
+  long long n;              // float4 elements
+  int nsrc;
 };

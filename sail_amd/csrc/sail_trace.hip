@@ -1642,6 +1642,33 @@ extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArg
   A.accum[pix] = acc;
 }
 
+// ---- multi-device frame reduction without RCCL (a multi-device context whose devices are all one GPU) ----------
+// dst = ((src0 + src1) + src2) + ...: the sum of the ranks' frames in rank order
+extern "C" __global__ void __launch_bounds__(256) sail_sum_kernel(SailSumArgs A) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= A.n) return;
+  float4 v = A.src[0][i];
+  for (int k = 1; k < A.nsrc; k++) {
+    const float4 w = A.src[k][i];
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  }
+  A.dst[i] = v;
+}
+// AOV maps of a tile-partitioned rank hold -0 outside its tiles: x + (-0) == x for every x (+0, -0 and NaN
+// included), so the sum over ranks reproduces the owning rank's AOV bits exactly (a +0 fill would turn -0 into +0)
+extern "C" __global__ void __launch_bounds__(256) sail_negzero_unowned_kernel(float4* a, float4* b, int W, int H,
+                                                                             int rank, int world) {
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= W || y >= H) return;
+  const int tilesX = (W + 63) / 64;
+  const int tile = (y >> 6) * tilesX + (x >> 6);
+  if (tile % world == rank) return;
+  const float4 nz = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+  const size_t pix = (size_t)y * W + x;
+  if (a) a[pix] = nz;
+  if (b) b[pix] = nz;
+}
+
 // ---- display filter (fsrender.glsl + filter/*.glsl), W x H generalisation of the 512 x 512 pass ---------------------
 // Every map is sampled as the reference's frame textures are: LINEAR, default REPEAT wrap (webgl.js:153-156),
 // RGB (texture() returns alpha 1). The colour map is the mean image (SUM accumulators divided per texel).
@@ -1659,7 +1686,10 @@ D Tap tapAt(int W, int H, float u, float v) {
 }
 D V3 texel(const SailFilterArgs& A, const float4* img, bool mean, int x, int y) {
   const float4 v = img[(size_t)y * A.W + x];
-  if (mean && A.accumMode == 0) return v3(v.x / A.count, v.y / A.count, v.z / A.count);
+  if (mean && A.accumMode == 0) {  // each texel's own count (a reduced tile frame may mix counts; 0: unrendered)
+    const float cnt = v.w > 0.0f ? v.w : 1.0f;
+    return v3(v.x / cnt, v.y / cnt, v.z / cnt);
+  }
   return v3(v.x, v.y, v.z);
 }
 D V3 bilerp(V3 t00, V3 t10, V3 t01, V3 t11, float a, float b) {
@@ -1857,6 +1887,15 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
 }
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s) {
   hipLaunchKernelGGL(sail_accum_kernel, dim3(blocks), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_sum(const SailSumArgs& A, hipStream_t s) {
+  hipLaunchKernelGGL(sail_sum_kernel, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
+  return hipGetLastError();
+}
+hipError_t sail_launch_negzero_unowned(float4* a, float4* b, int W, int H, int rank, int world, hipStream_t s) {
+  hipLaunchKernelGGL(sail_negzero_unowned_kernel, dim3((W + 15) / 16, (H + 15) / 16), dim3(256), 0, s, a, b, W, H,
+                     rank, world);
   return hipGetLastError();
 }
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s) {

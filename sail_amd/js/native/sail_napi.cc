@@ -117,6 +117,24 @@ napi_value Create(napi_env env, napi_callback_info info) {
   NAPI_OK(napi_create_external(env, hd, finalizeHandle, nullptr, &ext));
   return ext;
 }
+// (W, H, Int32Array devices, flags): one context over several GPUs (sail_create_multi)
+napi_value CreateMulti(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!args(env, info, 4, a)) return nullptr;
+  int w, h, flags;
+  int32_t* dev;
+  size_t nd;
+  if (!getInt(env, a[0], &w) || !getInt(env, a[1], &h) || !getArray(env, a[2], napi_int32_array, &dev, &nd) ||
+      !getInt(env, a[3], &flags))
+    return nullptr;
+  sail_ctx* c = nullptr;
+  const int rc = sail_create_multi(&c, w, h, dev, (int)nd, (uint32_t)flags);
+  if (rc) return throwSail(env, "sail_create_multi", rc, nullptr);
+  Handle* hd = new Handle{c, w, h};
+  napi_value ext;
+  NAPI_OK(napi_create_external(env, hd, finalizeHandle, nullptr, &ext));
+  return ext;
+}
 napi_value Destroy(napi_env env, napi_callback_info info) {
   napi_value a[1];
   if (!args(env, info, 1, a)) return nullptr;
@@ -181,6 +199,10 @@ napi_value IntSetter(napi_env env, napi_callback_info info, int nargs, const cha
 napi_value SetAccumMode(napi_env env, napi_callback_info info) { return IntSetter(env, info, 1, "sail_set_accum_mode", nullptr, sail_set_accum_mode); }
 napi_value SetLaunchSamples(napi_env env, napi_callback_info info) { return IntSetter(env, info, 1, "sail_set_launch_samples", nullptr, sail_set_launch_samples); }
 napi_value SetPartition(napi_env env, napi_callback_info info) { return IntSetter(env, info, 3, "sail_set_partition", sail_set_partition, nullptr); }
+int setDebug3(sail_ctx* c, int opt, int val, int) { return sail_set_debug(c, opt, val); }
+napi_value SetDebug(napi_env env, napi_callback_info info) { return IntSetter(env, info, 2, "sail_set_debug", setDebug3, nullptr); }
+int reduce3(sail_ctx* c, int root, int, int) { return sail_reduce(c, root); }
+napi_value Reduce(napi_env env, napi_callback_info info) { return IntSetter(env, info, 1, "sail_reduce", reduce3, nullptr); }
 
 napi_value Render(napi_env env, napi_callback_info info) {
   napi_value a[5];
@@ -414,6 +436,9 @@ napi_value Init(napi_env env, napi_value exports) {
       {"deviceCount", 0, DeviceCount, 0, 0, 0, napi_enumerable, 0},
       {"abiVersion", 0, AbiVersion, 0, 0, 0, napi_enumerable, 0},
       {"create", 0, Create, 0, 0, 0, napi_enumerable, 0},
+      {"createMulti", 0, CreateMulti, 0, 0, 0, napi_enumerable, 0},
+      {"setDebug", 0, SetDebug, 0, 0, 0, napi_enumerable, 0},
+      {"reduce", 0, Reduce, 0, 0, 0, napi_enumerable, 0},
       {"destroy", 0, Destroy, 0, 0, 0, napi_enumerable, 0},
       {"setScene", 0, SetScene, 0, 0, 0, napi_enumerable, 0},
       {"updateObjects", 0, UpdateObjects, 0, 0, 0, napi_enumerable, 0},

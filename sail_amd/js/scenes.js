@@ -109,7 +109,78 @@ function allKinds() {
   return scene;
 }
 
+// ---- coverage scenes (round 2): every geometry as an AreaLight, zero / one primitive, Bilerp --------------
+// AreaLight accepts any geometry (src/scene/light.js:40-55). Disk, Sphere and Rectangle sample a point with a
+// pdf (disk.glsl:77-83, sphere.glsl:88-92, rectangle.glsl:65-70); Cube, Cone, Cylinder, Hyperboloid,
+// Paraboloid and Cornellbox return BLACK without writing pdf (cube.glsl:50-52 etc.): defined as pdf = 0.
+function areaGood() {
+  const scene = new Sail.Scene();
+  const matte = new Sail.Matte(0.7);
+  scene.add(new Sail.Cube([0, 0, -7], [5.56, 5.488, 5.592], matte, Sail.Color.WHITE));
+  scene.add(new Sail.AreaLight(new Sail.Disk([1.5, 5.3, 2.5], 0.5, 0.1, matte, Sail.Color.BLACK), [3, 3, 3]));
+  scene.add(new Sail.AreaLight(new Sail.Sphere([4.0, 4.6, 3.0], 0.3, matte, Sail.Color.WHITE), [4, 4, 4]));
+  scene.add(new Sail.AreaLight(new Sail.Rectangle([2.5, 5.47, 1.0], [3.2, 5.47, 1.8], matte, Sail.Color.BLACK), [2, 2, 2]));
+  scene.add(new Sail.Sphere([2.0, 1.0, 2.5], 1.0, new Sail.Matte(0.7), new Sail.Checkerboard2([1, 1, 1], [0.2, 0.2, 0.2], 0.1)));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+function areaBlack() {
+  const scene = new Sail.Scene();
+  const matte = new Sail.Matte(0.7);
+  // a mirror room: paths reach the lights' surfaces (finite radiance) besides the matte sphere and floor
+  // disk, whose light samples divide by the unwritten pdf (inf / NaN radiance)
+  scene.add(new Sail.Cube([0, 0, -7], [5.56, 5.488, 5.592], new Sail.Mirror(0.9), Sail.Color.WHITE));
+  scene.add(new Sail.Disk([2.0, 0.01, 1.0], 1.2, 0.0, matte, Sail.Color.WHITE));
+  scene.add(new Sail.AreaLight(new Sail.Cube([0.5, 4.5, 3.0], [1.0, 5.0, 3.5], matte, Sail.Color.WHITE), [2, 2, 2]));
+  scene.add(new Sail.AreaLight(new Sail.Cone([1.5, 4.0, 3.0], 0.8, 0.4, matte, Sail.Color.WHITE), [2, 2, 2]));
+  scene.add(new Sail.AreaLight(new Sail.Cylinder([2.5, 4.0, 3.0], 0.8, 0.3, matte, Sail.Color.WHITE), [2, 2, 2]));
+  scene.add(new Sail.AreaLight(new Sail.Hyperboloid([3.5, 4.0, 3.0], [0.3, 0, 0], [0.15, 0.15, 0.8], matte, Sail.Color.WHITE), [2, 2, 2]));
+  scene.add(new Sail.AreaLight(new Sail.Paraboloid([4.5, 4.0, 3.0], 0, 0.8, 0.4, matte, Sail.Color.WHITE), [2, 2, 2]));
+  scene.add(new Sail.AreaLight(new Sail.Cornellbox([0.2, 0.2, 4.0], [1.0, 1.0, 4.8]), [2, 2, 2]));
+  scene.add(new Sail.Sphere([2.5, 1.0, 2.0], 0.8, matte, Sail.Color.WHITE));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// n = 1: the row coordinate float(i)/float(n-1) is 0/0 (shader.shape.js:34): row 0. A closed room (every ray
+// hits) with a point light (ln = 1), and a lone emissive sphere (rays around it miss)
+function oneRoom() {
+  const scene = new Sail.Scene();
+  scene.add(new Sail.Cube([0, 0, -7], [5.56, 5.488, 5.592], new Sail.Matte(0.7), new Sail.Checkerboard(0.1, 0.01)));
+  scene.add(new Sail.PointLight([2.78, 5, 2], [3, 3, 3]));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+function oneSphere() {
+  const scene = new Sail.Scene();
+  scene.add(new Sail.Sphere([2.78, 2.73, 2.79], 1.5, new Sail.Matte(0.7), Sail.Color.WHITE, [0.5, 0.8, 1.0]));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// n = 0: every primary ray misses (the AOV miss branch), with a light row that is never sampled
+function emptyScene() {
+  const scene = new Sail.Scene();
+  scene.add(new Sail.PointLight([2.78, 5, 2], [3, 3, 3]));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// Bilerp (bilerp.glsl:1-13; the reference's GLSL does not compile, the intended bilinear math is built) on
+// shapes with different UV maps
+function bilerpScene() {
+  const scene = new Sail.Scene();
+  const matte = new Sail.Matte(0.7);
+  const bl = () => new Sail.Bilerp([1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 1, 0]);
+  scene.add(new Sail.AreaLight(new Sail.Rectangle([2.13, 5.48, 2.27], [3.43, 5.48, 3.32], matte, Sail.Color.BLACK), [4, 4, 4]));
+  scene.add(new Sail.Cornellbox([0, 0, -7], [5.56, 5.488, 5.592]));
+  scene.add(new Sail.Sphere([1.2, 1.0, 2.5], 0.9, matte, bl()));
+  scene.add(new Sail.Cube([2.4, 0.0, 1.5], [3.3, 1.2, 2.4], matte, bl()));
+  scene.add(new Sail.Cylinder([4.2, 0.0, 2.5], 1.5, 0.6, matte, bl()));
+  scene.add(new Sail.Disk([2.78, 0.01, 3.8], 1.0, 0.2, matte, bl()));
+  scene.add(new Sail.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+
 const SCENES = {
   C1: () => readmeCornell(false), C1g: () => readmeCornell(true), C3: materialsDemo, C4: random64, UI: uiDemo, ALL: allKinds,
+  AREA: areaGood, AREA0: areaBlack, N1: oneRoom, N1S: oneSphere, N0: emptyScene, BILERP: bilerpScene,
 };
 module.exports = { SCENES, readmeCornell, materialsDemo, random64, uiDemo, allKinds };

@@ -1,6 +1,8 @@
 'use strict';
 // Sail.Renderer over libsail_hip.so (through the N-API addon) in place of the WebGL2 programs.
-//   new Renderer(canvas | {width, height, device, ...})   src/core/renderer.js:9-39
+//   new Renderer(canvas | {width, height, device, devices, ...})   src/core/renderer.js:9-39
+//     devices: N (GPUs 0..N-1) or an array of ordinals -> one multi-device context (sail_create_multi): the
+//     frame's tiles are dealt across the GPUs and summed into GPU 0 (RCCL) before each display / readback
 //   renderer.update(scene)        -> Tracer.update (tracer.js:42-90): rows + plugin set -> sail_set_scene
 //   renderer.updateObjects(scene) -> Tracer.updateObjects (tracer.js:25-40) -> sail_update_objects
 //   renderer.render(scene)        -> Tracer.render (tracer.js:92-101): one progressive sample with a
@@ -36,13 +38,19 @@ class Renderer {
     this.width = opts.width || (this.canvas && this.canvas.width) || 512;    // webgl.js:24 (512 x 512)
     this.height = opts.height || (this.canvas && this.canvas.height) || 512;
     this.device = opts.device === undefined ? -1 : opts.device;
+    this.devices = opts.devices === undefined ? null
+      : (Array.isArray(opts.devices) ? opts.devices.slice() : Array.from({ length: opts.devices }, (_, i) => i));
+    if (this.devices && this.devices.length < 1) throw new Error('Renderer: devices must name at least one GPU');
     this.maxBounces = opts.maxBounces || MAXBOUNCES;
     this.deterministic = !!opts.deterministic;  // frozen schedule (SURVEY §8(d)) instead of Math.random + clock
     this.accumulation = opts.accumulation || 'mix';
     this.aov = opts.aov !== false;
     this.display = opts.display === undefined ? !!this.canvas : !!opts.display;
     this.lib = native.load();
-    this.ctx = this.lib.create(this.width, this.height, this.device, (this.aov ? 1 : 0) | 2);
+    const flags = (this.aov ? 1 : 0) | 2;
+    this.ctx = this.devices ? this.lib.createMulti(this.width, this.height, Int32Array.from(this.devices), flags)
+      : this.lib.create(this.width, this.height, this.device, flags);
+    if (opts.partition === 'samples') this.lib.setPartition(this.ctx, 0, 1, 1);
     this.lib.setAccumMode(this.ctx, ACCUM[this.accumulation]);
     this.timeStart = Date.now();
     this.filter = filterConfig({ name: 'color', params: {} });

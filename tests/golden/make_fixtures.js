@@ -156,6 +156,76 @@ function sceneAllTextures() {  // every texture / material kind once (Bilerp exc
   return scene;
 }
 
+// ---- coverage scenes (round 2): every geometry as an AreaLight, zero / one primitive, Bilerp --------------
+// AreaLight accepts any geometry (src/scene/light.js:40-55). Disk, Sphere and Rectangle sample a point with a
+// pdf (disk.glsl:77-83, sphere.glsl:88-92, rectangle.glsl:65-70); Cube, Cone, Cylinder, Hyperboloid,
+// Paraboloid and Cornellbox return BLACK without writing pdf (cube.glsl:50-52 etc.): defined as pdf = 0.
+function sceneAreaGood() {
+  const scene = new S.Scene();
+  const matte = new S.Matte(0.7);
+  scene.add(new S.Cube([0, 0, -7], [5.56, 5.488, 5.592], matte, S.Color.WHITE));
+  scene.add(new S.AreaLight(new S.Disk([1.5, 5.3, 2.5], 0.5, 0.1, matte, S.Color.BLACK), [3, 3, 3]));
+  scene.add(new S.AreaLight(new S.Sphere([4.0, 4.6, 3.0], 0.3, matte, S.Color.WHITE), [4, 4, 4]));
+  scene.add(new S.AreaLight(new S.Rectangle([2.5, 5.47, 1.0], [3.2, 5.47, 1.8], matte, S.Color.BLACK), [2, 2, 2]));
+  scene.add(new S.Sphere([2.0, 1.0, 2.5], 1.0, new S.Matte(0.7), new S.Checkerboard2([1, 1, 1], [0.2, 0.2, 0.2], 0.1)));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+function sceneAreaBlack() {
+  const scene = new S.Scene();
+  const matte = new S.Matte(0.7);
+  // a mirror room: paths reach the lights' surfaces (finite radiance) besides the matte sphere and floor
+  // disk, whose light samples divide by the unwritten pdf (inf / NaN radiance)
+  scene.add(new S.Cube([0, 0, -7], [5.56, 5.488, 5.592], new S.Mirror(0.9), S.Color.WHITE));
+  scene.add(new S.Disk([2.0, 0.01, 1.0], 1.2, 0.0, matte, S.Color.WHITE));
+  scene.add(new S.AreaLight(new S.Cube([0.5, 4.5, 3.0], [1.0, 5.0, 3.5], matte, S.Color.WHITE), [2, 2, 2]));
+  scene.add(new S.AreaLight(new S.Cone([1.5, 4.0, 3.0], 0.8, 0.4, matte, S.Color.WHITE), [2, 2, 2]));
+  scene.add(new S.AreaLight(new S.Cylinder([2.5, 4.0, 3.0], 0.8, 0.3, matte, S.Color.WHITE), [2, 2, 2]));
+  scene.add(new S.AreaLight(new S.Hyperboloid([3.5, 4.0, 3.0], [0.3, 0, 0], [0.15, 0.15, 0.8], matte, S.Color.WHITE), [2, 2, 2]));
+  scene.add(new S.AreaLight(new S.Paraboloid([4.5, 4.0, 3.0], 0, 0.8, 0.4, matte, S.Color.WHITE), [2, 2, 2]));
+  scene.add(new S.AreaLight(new S.Cornellbox([0.2, 0.2, 4.0], [1.0, 1.0, 4.8]), [2, 2, 2]));
+  scene.add(new S.Sphere([2.5, 1.0, 2.0], 0.8, matte, S.Color.WHITE));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// n = 1: the row coordinate float(i)/float(n-1) is 0/0 (shader.shape.js:34): row 0. A closed room (every ray
+// hits) with a point light (ln = 1), and a lone emissive sphere (rays around it miss)
+function sceneOneRoom() {
+  const scene = new S.Scene();
+  scene.add(new S.Cube([0, 0, -7], [5.56, 5.488, 5.592], new S.Matte(0.7), new S.Checkerboard(0.1, 0.01)));
+  scene.add(new S.PointLight([2.78, 5, 2], [3, 3, 3]));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+function sceneOneSphere() {
+  const scene = new S.Scene();
+  scene.add(new S.Sphere([2.78, 2.73, 2.79], 1.5, new S.Matte(0.7), S.Color.WHITE, [0.5, 0.8, 1.0]));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// n = 0: every primary ray misses (the AOV miss branch), with a light row that is never sampled
+function sceneEmpty() {
+  const scene = new S.Scene();
+  scene.add(new S.PointLight([2.78, 5, 2], [3, 3, 3]));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+// Bilerp (bilerp.glsl:1-13; the reference's GLSL does not compile, the intended bilinear math is built) on
+// shapes with different UV maps
+function sceneBilerp() {
+  const scene = new S.Scene();
+  const matte = new S.Matte(0.7);
+  const bl = () => new S.Bilerp([1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 1, 0]);
+  scene.add(new S.AreaLight(new S.Rectangle([2.13, 5.48, 2.27], [3.43, 5.48, 3.32], matte, S.Color.BLACK), [4, 4, 4]));
+  scene.add(new S.Cornellbox([0, 0, -7], [5.56, 5.488, 5.592]));
+  scene.add(new S.Sphere([1.2, 1.0, 2.5], 0.9, matte, bl()));
+  scene.add(new S.Cube([2.4, 0.0, 1.5], [3.3, 1.2, 2.4], matte, bl()));
+  scene.add(new S.Cylinder([4.2, 0.0, 2.5], 1.5, 0.6, matte, bl()));
+  scene.add(new S.Disk([2.78, 0.01, 3.8], 1.0, 0.2, matte, bl()));
+  scene.add(new S.Camera([2.78, 2.73, -6], [2.78, 2.73, 2.79]));
+  return scene;
+}
+
 function capture(name, scene) {
   const renderer = new S.Renderer(canvas);
   const c0 = calls.length;
@@ -200,6 +270,12 @@ out.scenes.C3 = capture('C3', sceneC3());
 out.scenes.C4 = capture('C4', sceneC4());
 out.scenes.UI = capture('UI', sceneUI());
 out.scenes.ALL = capture('ALL', sceneAllTextures());
+out.scenes.AREA = capture('AREA', sceneAreaGood());
+out.scenes.AREA0 = capture('AREA0', sceneAreaBlack());
+out.scenes.N1 = capture('N1', sceneOneRoom());
+out.scenes.N1S = capture('N1S', sceneOneSphere());
+out.scenes.N0 = capture('N0', sceneEmpty());
+out.scenes.BILERP = capture('BILERP', sceneBilerp());
 
 // ---- box / triangle / mitchell tables through the same codegen ----------------------------------
 out.filters = {};

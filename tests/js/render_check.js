@@ -1,7 +1,9 @@
 'use strict';
 // Renders a frozen scene through Sail.Renderer -> N-API -> libsail_hip.so and writes the raw accumulator
 // (and the canvas pixels) for tests/test_js_host.py to compare with the CPU oracle. Needs an MI355X.
-// argv: scene W H spp bounces mode(sum|mix) api(samples|frames) out_prefix [filter [filter-r]]
+// argv: scene W H spp bounces mode(sum|mix) api(samples|frames|progressive) out_prefix [filter [filter-r]]
+// env SAIL_TEST_DEVICES=0,0,0: a multi-device Renderer ({devices: [...]}); progressive = half the samples as
+// frames, a display pass (reduces the devices' frames), the other half, then the readback
 const fs = require('fs');
 const Sail = require('../../sail_amd/js');
 const { SCENES } = require('../../sail_amd/js/scenes');
@@ -11,10 +13,17 @@ if (filter) {  // the reference's scene.filter = name; scene.filter.addParam('r'
   scene.filter = filter;
   if (filterR) scene.filter.addParam('r', filterR);
 }
-const r = new Sail.Renderer({ width: +W, height: +H, deterministic: true, accumulation: mode, maxBounces: +B, display: false });
+const devices = process.env.SAIL_TEST_DEVICES ? process.env.SAIL_TEST_DEVICES.split(',').map(Number) : undefined;
+const r = new Sail.Renderer({ width: +W, height: +H, deterministic: true, accumulation: mode, maxBounces: +B, display: false,
+  devices });
 r.update(scene);
 if (api === 'samples') r.renderSamples(scene, +spp);
-else for (let i = 0; i < +spp; i++) r.render(scene);
+else if (api === 'progressive') {
+  const half = Math.floor(+spp / 2);
+  for (let i = 0; i < half; i++) r.render(scene);
+  r.image();
+  for (let i = half; i < +spp; i++) r.render(scene);
+} else for (let i = 0; i < +spp; i++) r.render(scene);
 fs.writeFileSync(out + '.accum.f32', Buffer.from(r.readAccum().buffer));
 fs.writeFileSync(out + '.rgba8', Buffer.from(r.image().buffer));
 if (filter) {

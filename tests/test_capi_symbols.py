@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert capi.load().sail_abi_version() == 1
+    assert capi.load().sail_abi_version() == 2
 
 
 def test_library_targets_gfx950():
@@ -56,6 +56,10 @@ def test_device_entry_points_fail_loudly_without_gpu():
         pytest.skip("a device is present")
     with pytest.raises(capi.SailError):
         capi.Context(16, 16)
+    with pytest.raises(capi.SailError):
+        capi.Context(16, 16, devices=[0, 0])
+    with pytest.raises(capi.SailError):
+        capi.Context(16, 16, devices=[0, 1, 0])   # neither all distinct nor all the same device
 
 
 def test_bad_arguments_are_rejected():
@@ -65,3 +69,11 @@ def test_bad_arguments_are_rejected():
     null = capi._ptr(None, ctypes.c_int)
     assert lib.sail_partition_tiles(0, 10, 0, 1, null, 0) < 0
     assert lib.sail_partition_tiles(10, 10, 2, 2, null, 0) < 0
+
+
+def test_null_context_is_rejected():
+    lib = capi.load()
+    for fn in ("sail_reset", "sail_sync"):
+        assert getattr(lib, fn)(None) == -1
+    assert lib.sail_set_debug(None, capi.DEBUG_CULL_MIN_PRIMS, 0) == -1
+    assert lib.sail_reduce(None, 0) == -1

@@ -79,14 +79,14 @@ def test_c4_precull_conservative_full_frame(frozen, monkeypatch, fused):
     bit for bit (every pixel, 2 samples, 12 bounces; tools/cull_check.py), in the fused slab form the library
     picks for this scene and in the plain form (SAIL_CULL_FMA=0). C4's bounce rays include about 1.4 M
     axis-parallel ones per sample (a zero direction component, infinite reciprocal)."""
-    monkeypatch.setenv("SAIL_CULL_FMA", fused)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_FMA, int(fused))
     sc = frozen["C4"]
     W, H, B, spp = 3840, 2160, 12, 2
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     out = {}
     for cull in ("0", "1000"):
-        monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+        monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, int(cull))
         ctx = capi.Context(W, H)
         ctx.set_scene_dict(sc)
         ctx.render_schedule(inv, seeds, sc["eye"], B)
@@ -142,7 +142,7 @@ def test_c4_precull_far_origins(frozen, monkeypatch, variant):
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     out = {}
     for cull in ("0", "1000"):
-        monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+        monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, int(cull))
         ctx = capi.Context(W, H)
         ctx.set_scene_dict(sc)
         ctx.render_schedule(inv, seeds, sc["eye"], B)

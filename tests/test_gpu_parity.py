@@ -191,6 +191,7 @@ def _weights(fixtures, name):
     (capi.FILTER_COLOR, None, 0, 2.2), (capi.FILTER_GAMMA, None, 0, 2.2), (capi.FILTER_TONEMAPPING, None, 0, 2.2),
     (capi.FILTER_WINDOW, "gaussian", (1.5, 2.5), 2.2), (capi.FILTER_WINDOW, "sinc", (3.0, 3.0), 2.2),
     (capi.FILTER_WINDOW, "box", (1.5, 1.5), 2.2), (capi.FILTER_WINDOW, "mitchell", (2.0, 2.0), 2.2),
+    (capi.FILTER_WINDOW, "triangle", (2.0, 2.0), 2.2), (capi.FILTER_GAMMA, None, 0, 1.8),
 ])
 def test_filter_bit_exact(gpu, fixtures, kind, fname, r, gamma):
     sc = fixtures["scenes"]["C3"]
@@ -216,7 +217,7 @@ def test_filter_bit_exact(gpu, fixtures, kind, fname, r, gamma):
 def test_update_objects_and_reset(gpu, fixtures, monkeypatch, cull):
     """Tracer.updateObjects path (tracer.js:25-40): new rows, accumulation restarts (with the pre-cull kernel
     forced on, the candidate sweep's per-chunk type masks are re-uploaded with the rows)."""
-    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, int(cull))
     sc = fixtures["scenes"]["C1"]
     W, H = 32, 32
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, 2)
@@ -299,7 +300,7 @@ def test_pick_matches_oracle(gpu, fixtures, name):
                                             ("UI", 32, 32, 3, 5), ("C4", 24, 24, 2, 12)])
 @pytest.mark.parametrize("cull", ["0", "1000"])
 def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, B, cull):
-    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)   # 0: cull every scene, 1000: never
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, int(cull))   # 0: cull every scene, 1000: never
     got, want, st, segs, _, _ = _render_both(fixtures, name, W, H, spp, B, launch=2)
     assert bit_equal(got, want).all()
     assert st.segments == segs
@@ -309,7 +310,7 @@ def test_precull_forced_on_and_off(gpu, fixtures, monkeypatch, name, W, H, spp, 
 # so equal distances from different rows are everywhere: the lower row must win, as in the in-order sweep ------
 @pytest.mark.parametrize("cull", ["0", "1000"])
 def test_candidate_sweep_chunks_and_ties(gpu, fixtures, monkeypatch, cull):
-    monkeypatch.setenv("SAIL_CULL_MIN_PRIMS", cull)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, int(cull))
     sc = dict(fixtures["scenes"]["C4"])
     sc["objects"] = list(sc["objects"]) * 2
     sc["n"] = 2 * sc["n"]                       # 134 rows: chunks of 64, 64, 6
@@ -323,7 +324,7 @@ def test_candidate_sweep_chunks_and_ties(gpu, fixtures, monkeypatch, cull):
 # ---- plugin-set kernels: the Cornell-box kernel (C1 scenes by default) and the generic one agree bit for bit --
 @pytest.mark.parametrize("force", ["0", "1"])
 def test_plugin_set_kernels(gpu, fixtures, monkeypatch, force):
-    monkeypatch.setenv("SAIL_FORCE_GENERIC", force)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_FORCE_GENERIC, int(force))
     got, want, st, segs, _, _ = _render_both(fixtures, "C1", 56, 40, 4, 6, launch=3)
     assert bit_equal(got, want).all()
     assert st.segments == segs
@@ -345,7 +346,7 @@ def test_kernel_selection(gpu, fixtures):
 @pytest.mark.parametrize("groups", ["1", "2", "5"])
 @pytest.mark.parametrize("mode", [capi.ACCUM_SUM, capi.ACCUM_MIX])
 def test_sample_groups(gpu, fixtures, monkeypatch, name, groups, mode):
-    monkeypatch.setenv("SAIL_SAMPLE_GROUPS", groups)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_SAMPLE_GROUPS, int(groups))
     got, want, st, segs, gaov, waov = _render_both(fixtures, name, 40, 24, 7, 5, mode=mode, aov=True, launch=7)
     assert bit_equal(got, want).all()
     assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
@@ -440,3 +441,44 @@ def test_unusual_viewpoints(gpu, fixtures, label, eye, center):
     assert bit_equal(got, want).all(), label
     assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all(), label
     assert st.segments == segs, label
+
+
+# ---- coverage scenes (tests/golden/make_fixtures.js, rows from the reference serializer) ---------------------------
+# AREA: Disk / Sphere / Rectangle area lights (sampled with a pdf); AREA0: Cube / Cone / Cylinder / Hyperboloid /
+# Paraboloid / Cornellbox area lights, whose samplers never write pdf (cube.glsl:50-52 ...; defined as 0, so their
+# light samples are inf / NaN, which must match bit for bit too); N1 / N1S: one primitive (row coordinate 0/0);
+# N0: no primitive (every primary ray misses); BILERP: the Bilerp texture on four UV maps
+COVERAGE = [("AREA", 40, 32, 4, 6), ("AREA0", 40, 32, 1, 1), ("AREA0", 40, 32, 2, 3), ("AREA0", 32, 24, 4, 8),
+            ("N1", 40, 32, 4, 6), ("N1S", 40, 32, 4, 5), ("N0", 24, 16, 2, 5), ("BILERP", 40, 32, 4, 6)]
+
+
+@pytest.mark.parametrize("name,W,H,spp,B", COVERAGE)
+@pytest.mark.parametrize("kernel", ["default", "generic", "cull"])
+def test_coverage_scenes_bit_exact(gpu, fixtures, monkeypatch, name, W, H, spp, B, kernel):
+    if kernel == "generic":
+        monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_FORCE_GENERIC, 1)
+        monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, 1000)
+    elif kernel == "cull":
+        monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, 0)
+    got, want, st, segs, gaov, waov = _render_both(fixtures, name, W, H, spp, B, aov=True, launch=3)
+    same = bit_equal(got, want)
+    assert same.all(), f"{name}: {int((~same).sum())} channels differ"
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
+    fin = np.isfinite(want[..., :3])
+    if name == "AREA0":   # the pdf-less samplers: inf / NaN where a matte vertex sampled one, finite elsewhere
+        assert (~fin).any() and fin.mean() > 0.5
+    else:
+        assert fin.all()
+    if name == "N0":
+        assert (want[..., :3] == 0).all() and segs == W * H * spp
+
+
+def test_coverage_kernel_selection(gpu, fixtures):
+    want = {"AREA": "sail_trace_kernel", "AREA0": "sail_trace_kernel_cull", "N1": "sail_trace_kernel_room",
+            "N1S": "sail_trace_kernel_cornell", "N0": "sail_trace_kernel_room", "BILERP": "sail_trace_kernel"}
+    for name, k in want.items():
+        ctx = capi.Context(8, 8)
+        ctx.set_scene_dict(fixtures["scenes"][name])
+        assert ctx.kernel_name() == k, name
+        ctx.close()

@@ -30,7 +30,7 @@ def bits(a):
     return np.asarray(a, dtype=np.float32).view(np.uint32)
 
 
-@pytest.mark.parametrize("name", ["C1", "C1g", "C3", "C4", "UI", "ALL"])
+@pytest.mark.parametrize("name", ["C1", "C1g", "C3", "C4", "UI", "ALL", "AREA", "AREA0", "N1", "N1S", "N0", "BILERP"])
 def test_scene_rows_match_reference_serializer(fixtures, exported, name):
     mine, ref = exported[name], fixtures["scenes"][name]
     for k in ("n", "tn", "ln", "plugins", "eye"):
@@ -77,17 +77,23 @@ def test_renderer_fails_loudly_without_device():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,W,H,spp,B,mode,api", [
-    ("C1", 40, 30, 4, 5, "sum", "samples"),
-    ("C3", 32, 32, 3, 5, "mix", "frames"),
-    ("UI", 24, 24, 2, 5, "mix", "samples"),
+@pytest.mark.parametrize("name,W,H,spp,B,mode,api,devices", [
+    ("C1", 40, 30, 4, 5, "sum", "samples", None),
+    ("C3", 32, 32, 3, 5, "mix", "frames", None),
+    ("UI", 24, 24, 2, 5, "mix", "samples", None),
+    # new Sail.Renderer({devices: [...]}): one multi-device context; progressive frames with a display pass
+    # (a reduce into device 0) between them (on one MI355X every "device" is GPU 0)
+    ("C1", 150, 70, 4, 5, "sum", "progressive", "0"),
+    ("C3", 150, 70, 4, 5, "sum", "progressive", "0,0,0"),
+    ("UI", 130, 66, 4, 5, "mix", "progressive", "0,0"),
 ])
-def test_js_renderer_bit_exact_vs_oracle(tmp_path, fixtures, exported, name, W, H, spp, B, mode, api):
+def test_js_renderer_bit_exact_vs_oracle(tmp_path, fixtures, exported, name, W, H, spp, B, mode, api, devices):
     if capi.device_count() < 1:
         pytest.skip("no HIP device")
     prefix = str(tmp_path / name)
+    env = dict(os.environ, **({"SAIL_TEST_DEVICES": devices} if devices else {}))
     subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "render_check.js"), name, str(W), str(H), str(spp), str(B),
-                    mode, api, prefix], cwd=ROOT, check=True, timeout=300)
+                    mode, api, prefix], cwd=ROOT, check=True, timeout=300, env=env)
     got = np.fromfile(prefix + ".accum.f32", dtype=np.float32).reshape(H, W, 4)
     sc = exported[name]
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)

@@ -1,7 +1,9 @@
 """CPU, world_size 2 over gloo: the multi-GPU data path (64x64 tiles dealt t % world, each rank's float4
-accumulator zero outside its tiles, one sum-reduce into rank 0) reproduces the single-rank frame bit for
-bit. The ranks render with the CPU oracle here; on MI355X the same partition runs through
-sail_set_partition + sail_reduce (RCCL) and tests/test_gpu_parity.py checks the tile split on one device."""
+accumulator zero outside its tiles, a sum-reduce into a separate frame on rank 0) reproduces the single-rank
+frame bit for bit, also progressively (render -> reduce -> render -> reduce: every reduce sums the ranks'
+cumulative accumulators afresh, as sail_reduce does). The ranks render with the CPU oracle here; on MI355X the
+same partition runs through sail_set_partition + sail_reduce (RCCL) and tests/test_gpu_multi.py checks the
+product's reduce (multi-device context, RCCL at one rank) on one device."""
 import os
 import socket
 
@@ -21,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, sc, W, H, spp, B, mode, q):
+def _worker(rank, world, port, sc, W, H, spp, B, mode, q, progressive=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -34,30 +36,38 @@ def _worker(rank, world, port, sc, W, H, spp, B, mode, q):
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
     masks = capi.plugin_masks(sc["plugins"])
     acc = np.zeros((H, W, 4), np.float32)
-    if mode == "tiles":
-        for x0, y0, w, h in capi.partition_tiles(W, H, rank, world):
-            oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(int(x0), int(y0), int(w), int(h)), accum=acc)
-    else:  # sample split: rank takes samples k = rank (mod world)
-        sel = np.arange(spp) % world == rank
-        oracle.render(sc, masks, W, H, inv[sel], seeds[sel], sc["eye"], B, accum=acc)
-    t = torch.from_numpy(acc)
-    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    passes = [np.arange(spp) < spp // 2, np.arange(spp) >= spp // 2] if progressive else [np.ones(spp, bool)]
+    frames = []
+    for part in passes:
+        if mode == "tiles":
+            for x0, y0, w, h in capi.partition_tiles(W, H, rank, world):
+                oracle.render(sc, masks, W, H, inv[part], seeds[part], sc["eye"], B,
+                              crop=(int(x0), int(y0), int(w), int(h)), accum=acc)
+        else:  # sample split: rank takes samples k = rank (mod world)
+            sel = part & (np.arange(spp) % world == rank)
+            oracle.render(sc, masks, W, H, inv[sel], seeds[sel], sc["eye"], B, accum=acc)
+        # out of place: the accumulator stays this rank's own; the frame is rank 0's display copy
+        frame = torch.zeros((H, W, 4), dtype=torch.float32)
+        frame.copy_(torch.from_numpy(acc))
+        dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        frames.append(frame.numpy().copy())
     if rank == 0:
-        q.put(t.numpy().copy())
+        q.put(frames[-1])
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("progressive", [False, True])
 @pytest.mark.parametrize("mode", ["tiles", "samples"])
-def test_two_rank_reduce_equals_single_rank(fixtures, mode):
+def test_two_rank_reduce_equals_single_rank(fixtures, mode, progressive):
     import oracle
     from sail_amd import capi
     sc = fixtures["scenes"]["C3"]
-    W, H, spp, B = 130, 70, 2, 4
+    W, H, spp, B = 130, 70, 4 if progressive else 2, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sc, W, H, spp, B, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sc, W, H, spp, B, mode, q, progressive)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Full-frame check that the pre-cull is conservative: the C4 frame (3840x2160, 12 bounces) rendered with the
-pre-cull kernel and with the pre-cull disabled (SAIL_CULL_MIN_PRIMS=1000: the in-order sweep over every row)
+pre-cull kernel and with the pre-cull disabled (DEBUG_CULL_MIN_PRIMS=1000: the in-order sweep over every row)
 must be bit-identical. Usage: tools/cull_check.py [spp] [library .so, default the in-tree build]"""
 import json
 import os
@@ -23,8 +23,7 @@ def main():
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     out = {}
     for cull in ("0", "1000"):
-        os.environ["SAIL_CULL_MIN_PRIMS"] = cull
-        ctx = capi.Context(W, H)
+        ctx = capi.Context(W, H, debug={capi.DEBUG_CULL_MIN_PRIMS: int(cull)})
         ctx.set_scene_dict(sc)
         ctx.render_schedule(inv, seeds, sc["eye"], B)
         out[cull] = ctx.read_accum()
