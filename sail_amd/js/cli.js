@@ -5,15 +5,15 @@
 //
 //   node sail_amd/js/cli.js scene.js [--width 512] [--height 512] [--spp 64] [--bounces 5] [--device -1]
 //        [--filter <name>] [--filter-r 'vec2(2.0,2.0)'] [--gamma 2.2] [--deterministic]
-//        [--png out.png] [--pfm out.pfm] [--stats]
+//        [--png out.png] [--pfm out.pfm] [--exr out.exr] [--stats]
 //
 // The script sees `Sail` (the full API) and must assign `scene` (a Sail.Scene with a camera), exactly as the
-// editor text does. --filter overrides scene.filter for the PNG; the PFM is always the unfiltered mean image.
+// editor text does. --filter overrides scene.filter for the PNG; the PFM and EXR are always the unfiltered mean image.
 const fs = require('fs');
 const path = require('path');
 const vm = require('vm');
 const Sail = require('./index');
-const { writePFM, writePNG } = require('./src/image');
+const { writePFM, writePNG, writeEXR } = require('./src/image');
 
 function parse(argv) {
   const opt = { width: 512, height: 512, spp: 64, bounces: 5, device: -1, deterministic: false, stats: false };
@@ -32,6 +32,7 @@ function parse(argv) {
       case '--gamma': opt.gamma = val(); break;
       case '--png': opt.png = val(); break;
       case '--pfm': opt.pfm = val(); break;
+      case '--exr': opt.exr = val(); break;
       case '--deterministic': opt.deterministic = true; break;
       case '--stats': opt.stats = true; break;
       case '-h': case '--help': opt.help = true; break;
@@ -72,6 +73,7 @@ function main() {
   const mean = r.readPixels();
   const ms = Number(process.hrtime.bigint() - t0) / 1e6;
   if (opt.pfm) writePFM(opt.pfm, opt.width, opt.height, mean);
+  if (opt.exr) writeEXR(opt.exr, opt.width, opt.height, mean);
   if (opt.png) writePNG(opt.png, opt.width, opt.height, r.image());
   if (opt.stats) {
     const st = r.stats();

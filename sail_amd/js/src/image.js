@@ -4,6 +4,9 @@
 //   PFM  — the float mean image (or any W x H x 4 float map), little-endian, rows bottom-to-top, which is
 //          exactly the GL row order the renderer already holds, so no flip.
 //   PNG  — the display-filtered RGBA8 canvas pixels (top-to-bottom rows, so the GL rows are flipped).
+//   EXR  — the float mean image as a single-part scanline OpenEXR file: channels B, G, R (the format sorts them by
+//          name) of 32-bit FLOAT, NO_COMPRESSION, one scanline per chunk, INCREASING_Y line order; EXR's y grows
+//          downwards, so the GL rows are flipped like the PNG's.
 const fs = require('fs');
 const zlib = require('zlib');
 
@@ -57,7 +60,53 @@ function toPNG(W, H, rgba8) {
     chunk('IDAT', zlib.deflateSync(raw)), chunk('IEND', Buffer.alloc(0))]);
 }
 
+// ---- OpenEXR (uncompressed scanline float) ----
+function exrAttr(name, type, value) {
+  const size = Buffer.alloc(4);
+  size.writeInt32LE(value.length, 0);
+  return Buffer.concat([Buffer.from(name + '\0' + type + '\0', 'ascii'), size, value]);
+}
+function i32s(...v) { const b = Buffer.alloc(4 * v.length); v.forEach((x, i) => b.writeInt32LE(x, 4 * i)); return b; }
+function f32s(...v) { const b = Buffer.alloc(4 * v.length); v.forEach((x, i) => b.writeFloatLE(x, 4 * i)); return b; }
+const EXR_FLOAT = 2;
+// rgba: W*H*4 floats in GL order (row 0 = bottom); the alpha slot (a sample count or 1) is not written
+function toEXR(W, H, rgba) {
+  const names = ['B', 'G', 'R'];            // chlist order is alphabetical; data follows it per scanline
+  const src = { R: 0, G: 1, B: 2 };
+  const chlist = Buffer.concat([...names.map((n) => Buffer.concat([Buffer.from(n + '\0', 'ascii'),
+    i32s(EXR_FLOAT), Buffer.from([0, 0, 0, 0]), i32s(1, 1)])), Buffer.from([0])]);
+  const header = Buffer.concat([
+    Buffer.from([0x76, 0x2f, 0x31, 0x01]), i32s(2),   // magic, version 2 (single-part scanline)
+    exrAttr('channels', 'chlist', chlist),
+    exrAttr('compression', 'compression', Buffer.from([0])),
+    exrAttr('dataWindow', 'box2i', i32s(0, 0, W - 1, H - 1)),
+    exrAttr('displayWindow', 'box2i', i32s(0, 0, W - 1, H - 1)),
+    exrAttr('lineOrder', 'lineOrder', Buffer.from([0])),
+    exrAttr('pixelAspectRatio', 'float', f32s(1)),
+    exrAttr('screenWindowCenter', 'v2f', f32s(0, 0)),
+    exrAttr('screenWindowWidth', 'float', f32s(1)),
+    Buffer.from([0])]);
+  const lineBytes = W * names.length * 4;
+  const chunkBytes = 8 + lineBytes;
+  const table = Buffer.alloc(8 * H);
+  const body = Buffer.alloc(chunkBytes * H);
+  const base = header.length + table.length;
+  for (let y = 0; y < H; y++) {
+    table.writeBigUInt64LE(BigInt(base + y * chunkBytes), 8 * y);
+    let o = y * chunkBytes;
+    body.writeInt32LE(y, o);
+    body.writeInt32LE(lineBytes, o + 4);
+    o += 8;
+    const row = (H - 1 - y) * W;
+    for (const n of names) {
+      for (let x = 0; x < W; x++, o += 4) body.writeFloatLE(rgba[4 * (row + x) + src[n]], o);
+    }
+  }
+  return Buffer.concat([header, table, body]);
+}
+
 function writePFM(path, W, H, rgba) { fs.writeFileSync(path, toPFM(W, H, rgba)); }
 function writePNG(path, W, H, rgba8) { fs.writeFileSync(path, toPNG(W, H, rgba8)); }
+function writeEXR(path, W, H, rgba) { fs.writeFileSync(path, toEXR(W, H, rgba)); }
 
-module.exports = { toPFM, toPNG, writePFM, writePNG, crc32 };
+module.exports = { toPFM, toPNG, toEXR, writePFM, writePNG, writeEXR, crc32 };
