@@ -51,7 +51,7 @@ def load_scene(name="C1"):
         return json.load(f)[name]
 
 
-def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1):
+def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1, spp=8, full=False):
     """BASELINE.json's CPU baseline: the single-threaded JS/Node software shader (oracle/sail_soft.js, bit-exact
     with the C++ oracle and the HIP kernel) timed on the host on a bounded sample of the same frame: 32x32
     crops spiralling out from the centre, 8 spp each, until ~budget_s of render time (node start excluded).
@@ -62,12 +62,15 @@ def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1):
     node = shutil.which("node") or shutil.which("nodejs")
     if node is None:
         return None
-    spp, c = 8, 32
+    c = 32
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     cx, cy = (W - c) // 2, (H - c) // 2
-    offsets = sorted(((dx, dy) for dx in range(-30, 31) for dy in range(-17, 18)), key=lambda d: d[0] ** 2 + d[1] ** 2)
-    crops = [[cx + dx * c, cy + dy * c, c, c] for dx, dy in offsets
-             if 0 <= cx + dx * c and 0 <= cy + dy * c and cx + dx * c + c <= W and cy + dy * c + c <= H]
+    if full:  # the whole frame (W and H multiples of 32), no time budget
+        crops, budget_s = [[x, y, c, c] for y in range(0, H, c) for x in range(0, W, c)], 1e9
+    else:
+        offsets = sorted(((dx, dy) for dx in range(-30, 31) for dy in range(-17, 18)), key=lambda d: d[0] ** 2 + d[1] ** 2)
+        crops = [[cx + dx * c, cy + dy * c, c, c] for dx, dy in offsets
+                 if 0 <= cx + dx * c and 0 <= cy + dy * c and cx + dx * c + c <= W and cy + dy * c + c <= H]
     job = {"objects": sc["objects"], "n": sc["n"], "texparams": sc["texparams"], "tn": sc["tn"], "lights": sc["lights"],
            "ln": sc["ln"], "masks": list(masks), "W": W, "H": H, "inv": [float(v) for v in inv.reshape(-1)],
            "seeds": [float(v) for v in seeds], "eye": sc["eye"], "spp": spp, "maxBounces": B, "accumMode": 0,
@@ -77,13 +80,25 @@ def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1):
         with open(jp, "w") as f:
             json.dump(job, f)
         out = subprocess.run([node, os.path.join(ROOT, "oracle", "sail_soft.js"), jp, os.path.join(td, "o")],
-                             capture_output=True, text=True, timeout=budget_s * 10 + 60, check=True).stdout
+                             capture_output=True, text=True, timeout=(600 if full else budget_s * 10 + 60), check=True).stdout
     r = json.loads(out.strip().splitlines()[-1])
     return {"value": r["segments"] / r["seconds"] / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "implementation": f"oracle/sail_soft.js on Node {r['node']}, "
                               + ("single thread" if threads == 1 else f"{threads} worker_threads"),
-            "sample": f"{r['crops']} centre-out {c}x{c} crops of the frame, {spp} spp x {B} bounces = {r['segments']} "
-                      f"segments (exact count) in {r['seconds']:.2f} s"}
+            "sample": (f"the whole {W}x{H} frame" if full else f"{r['crops']} centre-out {c}x{c} crops of the frame")
+                      + f", {spp} spp x {B} bounces = {r['segments']} segments (exact count) in {r['seconds']:.2f} s"}
+
+
+def cpu_baseline_c1_full():
+    """BASELINE.md's CPU plan: configs[0] (C1 = the README Cornell box at 256x256, 4 bounces, 64 spp,
+    16,777,216 segments) rendered in full by the single-threaded JS/Node software shader (~30 s)."""
+    sc = load_scene("C1")
+    W = H = 256
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    r = cpu_baseline_js(sc, capi.plugin_masks(sc["plugins"]), mvp, W, H, 4, spp=64, full=True)
+    if r:
+        r["config"] = "C1: README Cornell box, 256x256, 4 bounces, 64 spp (BASELINE.json configs[0]), in full"
+    return r
 
 
 def cpu_baseline(sc, masks, mvp, W, H, B, budget_s=10.0):
@@ -187,6 +202,7 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--launch-spp", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c1-full", action="store_true", help="skip the ~30 s full C1 render of the CPU baseline")
     ap.add_argument("--force-comm", action="store_true",
                     help="exercise the torch.distributed + RCCL reduce path even with one rank")
     args = ap.parse_args()
@@ -335,6 +351,8 @@ def main():
             nthr = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16 cores
             jsmt = cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=6.0, threads=nthr) if (js and nthr > 1) else None
             rec["cpu_baseline"] = dict(js, cpp_port=cpp, worker_threads=jsmt) if js else cpp
+            if js and not args.no_c1_full:
+                rec["cpu_baseline"]["c1_full"] = cpu_baseline_c1_full()
         print(json.dumps(rec), flush=True)
     ctx.close()
     if dist is not None:
