@@ -146,6 +146,12 @@ int sail_jitter_inverse(const double mvp_rowmajor[16], double jx, double jy, int
  * and jitter from xorshift32(0x5A11 + k). Fills spp x 16 matrices and spp seeds for k = k0 .. k0+spp-1. */
 int sail_schedule(const double mvp_rowmajor[16], int width, int height, int k0, int spp, float* inv_colmajor, float* seeds);
 
+/* Object3D.boundbox() (src/scene/geometry.js; the picker's pre-test, pickup.js:55-56), answered by the bounds the
+ * trace kernels' pre-cull tests: for each of the n object rows (18 floats, Appendix A wire format; tn = the
+ * texParams row count the rows index), 6 floats min.xyz, max.xyz of the padded box, +-inf where a primitive has no
+ * finite bound; a row whose category is not a shape gets an empty box (+inf, -inf). Host-only (no device). */
+int sail_prim_bounds(const float* objects, int n, int tn, float* out_minmax);
+
 /* ---- multi-GPU (one process per GPU): image tiles / sample split + RCCL sum-reduce of the accumulators ---- */
 int sail_comm_unique_id(char id[128]);
 /* a second call replaces the communicator */

@@ -34,7 +34,7 @@ EXPORTS = (
     "sail_render", "sail_render_schedule", "sail_reset", "sail_sync", "sail_readback", "sail_read_accum",
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
-    "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
+    "sail_prim_bounds", "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
     "sail_abi_version",
 )
 
@@ -118,6 +118,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_accum_device_ptr": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]),
         "sail_partition_tiles": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+        "sail_prim_bounds": (ctypes.c_int, [f32p, ctypes.c_int, ctypes.c_int, f32p]),
         "sail_math_probe": (ctypes.c_int, [ctypes.c_int, f32p, f32p, f32p, ctypes.c_int]),
         "sail_abi_version": (ctypes.c_int, []),
         "sail_pick": (ctypes.c_int, [vp, f32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), f32p]),
@@ -186,6 +187,20 @@ def partition_tiles(width: int, height: int, rank: int, world: int) -> np.ndarra
     out = np.zeros((max(n, 1), 4), dtype=np.int32)
     lib.sail_partition_tiles(width, height, rank, world, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), n)
     return out[:n]
+
+
+def prim_bounds(objects, n: int, tn: int) -> np.ndarray:
+    """Object3D.boundbox() answered by the pre-cull's padded bounds: (n, 2, 3) min / max per object row
+    (host-only, no device)."""
+    lib = load()
+    rows = _f32(objects).reshape(-1)
+    if rows.size < 18 * n:
+        raise SailError("prim_bounds: fewer than 18 floats per row")
+    out = np.zeros((max(n, 1), 6), dtype=np.float32)
+    rc = lib.sail_prim_bounds(_ptr(rows), n, tn, _ptr(out))
+    if rc:
+        raise SailError(f"sail_prim_bounds: {rc}")
+    return out[:n].reshape(n, 2, 3)
 
 
 def math_probe(fn: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:

@@ -1286,6 +1286,21 @@ int sail_reduce(sail_ctx* c, int root) {
   return SAIL_OK;
 }
 
+int sail_prim_bounds(const float* objects, int n, int tn, float* out) {
+  if (n < 0 || (n > 0 && (!objects || !out))) return SAIL_E_INVALID;
+  std::vector<SailPrim> prims;
+  int anyHit = 0;
+  decodePrims(objects, n, tn, ~0u, prims, &anyHit, nullptr);
+  for (int i = 0; i < n; i++) {
+    const SailPrim& p = prims[(size_t)i];
+    for (int k = 0; k < 3; k++) {
+      out[6 * i + k] = p.type ? p.a[18 + k] : INFINITY;
+      out[6 * i + 3 + k] = p.type ? p.a[21 + k] : -INFINITY;
+    }
+  }
+  return SAIL_OK;
+}
+
 int sail_partition_tiles(int width, int height, int rank, int world, int* out, int capacity) {
   if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || capacity < 0) return SAIL_E_INVALID;
   const int tx = (width + 63) / 64, ty = (height + 63) / 64;

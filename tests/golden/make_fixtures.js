@@ -226,6 +226,82 @@ function sceneBilerp() {
   return scene;
 }
 
+// ---- the reference picker (src/core/pickup.js:46-66) on a grid of 512x512-canvas mouse positions: its selection
+// (the object's row: scene.objects order = serialized row order), the distance object.intersect() returns for it,
+// the picker's own ray (Ray.generate, pickup.js:9-12), and whether the four positions 0.75 px away pick the same
+// object (away from silhouettes)
+function pickGrid(scene, step) {
+  S.Control.update(scene);                        // Control.pick = new Pickup(scene)
+  const picker = S.Control.pick;
+  const inv = scene.mat.inverse();
+  const rows = [];
+  const sel = () => scene.objects.indexOf(scene.select);
+  for (let y = step / 2; y < 512; y += step) {
+    for (let x = step / 2; x < 512; x += step) {
+      picker.pick(x, y);
+      const row = sel();
+      let stable = true;
+      for (const [dx, dy] of [[0.75, 0], [-0.75, 0], [0, 0.75], [0, -0.75]]) {
+        picker.pick(x + dx, y + dy);
+        if (sel() !== row) stable = false;
+      }
+      const dir = inv.multiply(new S.Vector([(x / 512) * 2 - 1, 1 - (y / 512) * 2, 0, 1])).divideByW().ensure3()
+        .subtract(scene.eye);
+      const t = row >= 0 ? scene.objects[row].intersect({ origin: scene.eye, dir }) : null;
+      // the ray as the f32 values sail_pick receives (Math.fround), t to 9 significant digits: data size
+      rows.push({ x, y, row, t: t === null ? null : +t.toPrecision(9), stable, dir: Array.from(dir.elements, Math.fround) });
+    }
+  }
+  return { eye: Array.from(scene.eye.elements), picks: rows };
+}
+// each object's boundbox() (src/scene/geometry.js: false for Object3D/Cornellbox, slack of 0.05 on flat axes)
+function boundboxes(scene) {
+  return scene.objects.map((o) => {
+    const b = o.boundbox();
+    return b ? { min: Array.from(b.min.elements), max: Array.from(b.max.elements), shape: o.constructor.name }
+      : { min: null, max: null, shape: o.constructor.name };
+  });
+}
+// the generated trace program's #defines (name -> value text) and the numeric literals of each of its functions,
+// as data: which constants the restatement must carry (tests/test_reference_constants.py)
+function programConstants(srcs) {
+  const prog = srcs.find((s) => /void trace\(/.test(s) && /intersectObjects/.test(s));
+  if (!prog) return null;
+  const defines = {};
+  const re = /^#define\s+(\w+)\s+(.*)$/gm;
+  let m;
+  while ((m = re.exec(prog))) defines[m[1]] = m[2].trim();
+  // function bodies by brace depth; a header is the text before a depth-0 '{'
+  const literals = {};
+  let depth = 0, fn = null, start = 0;
+  for (let i = 0; i < prog.length; i++) {
+    const ch = prog[i];
+    if (ch === '{') {
+      if (depth === 0) {
+        const head = prog.slice(start, i);
+        const h = /(\w+)\s*\([^()]*\)\s*$/.exec(head.replace(/\s+/g, ' '));
+        fn = h ? h[1] : null;
+        start = i + 1;
+      }
+      depth++;
+    } else if (ch === '}') {
+      depth--;
+      if (depth === 0) {
+        if (fn) {
+          const body = prog.slice(start, i).replace(/\/\/.*$/gm, '');
+          const lits = body.match(/(?<![\w.])(\d+\.\d*|\.\d+|\d+)([eE][-+]?\d+)?(?![\w.])/g) || [];
+          literals[fn] = Array.from(new Set((literals[fn] || []).concat(lits.filter((x) => /[.eE]/.test(x)))));
+        }
+        fn = null;
+        start = i + 1;
+      }
+    } else if (depth === 0 && ch === ';') {
+      start = i + 1;
+    }
+  }
+  return { defines, literals };
+}
+
 function capture(name, scene) {
   const renderer = new S.Renderer(canvas);
   const c0 = calls.length;
@@ -245,6 +321,7 @@ function capture(name, scene) {
     filter: { name: scene.filter.name, params: Object.assign({}, scene.filter.params) },
     mvp_rowmajor: mat, eye: Array.from(scene.eye.elements),
     glsl_sha256: srcs.map(sha), glsl_lines: srcs.map((s) => s.split('\n').length),
+    boundbox: boundboxes(scene),
   };
   // weight table as emitted into the render program (window filters only)
   for (const s of srcs) {
@@ -276,6 +353,17 @@ out.scenes.N1 = capture('N1', sceneOneRoom());
 out.scenes.N1S = capture('N1S', sceneOneSphere());
 out.scenes.N0 = capture('N0', sceneEmpty());
 out.scenes.BILERP = capture('BILERP', sceneBilerp());
+
+// ---- reference picker selections (pickup.js) and the trace program's constants ------------------------------
+out.pick = {};
+for (const [name, mk, step] of [['C1', () => sceneC1(false), 32], ['C3', sceneC3, 32], ['UI', sceneUI, 32], ['C4', sceneC4, 16]])
+  out.pick[name] = pickGrid(mk(), step);
+out.program_constants = {};
+for (const [name, mk] of [['C1', () => sceneC1(false)], ['C3', sceneC3], ['C4', sceneC4], ['ALL', sceneAllTextures]]) {
+  const c0 = calls.length;
+  new S.Renderer(canvas).update(mk());
+  out.program_constants[name] = programConstants(shaderSources(c0));
+}
 
 // ---- box / triangle / mitchell tables through the same codegen ----------------------------------
 out.filters = {};
