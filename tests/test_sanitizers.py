@@ -1,0 +1,130 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer over the host code (the reference has no native code;
+this build's host side is C++): the C-ABI library's host paths (sail_capi.cpp, sail_hostmath.cpp), the CPU oracle
+and the Node-API addon, built instrumented by tools/sanitize_build.sh (device code is never instrumented) and
+driven under clang's ASan runtime over the fixture scenes and hostile inputs (tests/sanitize/). A sanitizer
+report aborts the child; its results must also equal the plain builds' bit for bit."""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from sail_amd import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "build", "sanitize")
+RT = "/opt/rocm/lib/llvm/lib/clang"
+NODE = shutil.which("node") or shutil.which("nodejs")
+
+
+def _runtime():
+    for ver in sorted(os.listdir(RT)) if os.path.isdir(RT) else []:
+        p = os.path.join(RT, ver, "lib", "linux", "libclang_rt.asan-x86_64.so")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def _env():
+    rt = _runtime()
+    if rt is None or not shutil.which("/opt/rocm/bin/hipcc"):
+        pytest.skip("clang ASan runtime / hipcc not available")
+    if os.environ.get("LD_PRELOAD"):
+        pytest.skip("another preload is active; the ASan runtime must load first")
+    if not os.path.exists(os.path.join(OUT, "libsail_hip_asan.so")) or not os.path.exists(os.path.join(OUT, "libsail_oracle_asan.so")):
+        subprocess.run(["sh", os.path.join(ROOT, "tools", "sanitize_build.sh")], check=True, capture_output=True, timeout=900)
+    env = dict(os.environ, LD_PRELOAD=rt,
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               SAIL_ORACLE_LIB=os.path.join(OUT, "libsail_oracle_asan.so"),
+               SAIL_LIB_ASAN=os.path.join(OUT, "libsail_hip_asan.so"),
+               HIP_VISIBLE_DEVICES="")
+    return env
+
+
+@pytest.fixture(scope="module")
+def host_results(tmp_path_factory):
+    env = _env()
+    if capi.device_count() > 0:
+        pytest.skip("the host-only drive expects no device (sail_create must fail)")
+    out = str(tmp_path_factory.mktemp("asan") / "host.npz")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "sanitize", "run_host.py"), out], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr, r.stderr[-6000:]
+    return np.load(out)
+
+
+def _eq(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.dtype.kind == "f":
+        return a.shape == b.shape and np.array_equal(a.view(np.uint32 if a.dtype == np.float32 else np.uint64),
+                                                     b.view(np.uint32 if b.dtype == np.float32 else np.uint64))
+    return np.array_equal(a, b)
+
+
+def test_sanitized_oracle_equals_plain_oracle(host_results, fixtures):
+    """renders (3 accumulation modes + AOVs), filters and picks of 10 scenes, spec math on 65 k bit patterns"""
+    n = 0
+    for key in host_results.files:
+        name, _, rest = key.partition("_")
+        if rest in ("0", "1", "2") and name in fixtures["scenes"]:
+            sc = fixtures["scenes"][name]
+            W, H, spp, B = {"C1": (12, 10, 2, 5), "C3": (10, 8, 2, 8), "C4": (8, 8, 1, 12), "ALL": (10, 8, 2, 6),
+                            "AREA0": (8, 8, 2, 4), "N0": (6, 4, 1, 3), "N1": (8, 6, 2, 4), "N1S": (8, 6, 2, 4),
+                            "BILERP": (8, 8, 2, 5), "UI": (8, 8, 2, 5)}[name]
+            inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+            acc, an, ap = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B,
+                                        accum_mode=int(rest), aov=True)
+            assert _eq(host_results[key], np.stack([acc, an, ap])), key
+            n += 1
+    assert n == 30
+    rng = np.random.default_rng(4)
+    bits = rng.integers(0, 2 ** 32, 1 << 16, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 3.4e38, -3.4e38, 1e15, 1e16], np.float32)
+    xs = np.concatenate([bits, specials])
+    for fn in (0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14):
+        assert _eq(host_results[f"math_{fn}"], oracle.math(fn, xs, xs[::-1].copy())), fn
+
+
+def test_sanitized_library_host_paths_equal_plain(host_results, fixtures):
+    """camera / schedule host math, scene decode (all fixtures + 64 hostile rows) and tile partitions"""
+    for name in ("C1", "C3", "C4", "UI"):
+        sc = fixtures["scenes"][name]
+        assert _eq(host_results[f"{name}_camera"],
+                   capi.camera(sc["eye"], sc.get("center", [2.78, 2.73, 2.79]), [0, 1, 0], 55.0, 16 / 9, 1.0, 100.0))
+        inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), 1920, 1080, 5, 64)
+        assert _eq(host_results[f"{name}_schedule_inv"], inv) and _eq(host_results[f"{name}_schedule_seeds"], seeds)
+    for name, sc in fixtures["scenes"].items():
+        if sc["n"] > 0:
+            assert _eq(host_results[f"{name}_bounds"], capi.prim_bounds(sc["objects"], sc["n"], sc["tn"])), name
+    assert host_results["fuzz_bounds"].shape == (64, 2, 3)
+    assert _eq(host_results["tiles_1920_1080_8_3"], capi.partition_tiles(1920, 1080, 3, 8))
+
+
+def test_sanitized_napi_addon(tmp_path):
+    if NODE is None:
+        pytest.skip("node not installed")
+    env = _env()
+    addon = os.path.join(OUT, "sail_napi_asan.node")
+    if not os.path.exists(addon):
+        pytest.skip("node headers not available: no instrumented addon")
+    if capi.device_count() > 0:
+        pytest.skip("the host-only drive expects no device")
+    env["SAIL_NAPI"] = addon
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "sanitize", "run_napi.js")], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-6000:]
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr, r.stderr[-6000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(res["badThrown"]), res["badThrown"]
+    mvp = capi.camera([2.78, 2.73, -6], [2.78, 2.73, 2.79], [0, 1, 0], 55.0, 16 / 9, 1.0, 100.0)
+    assert _eq(np.array(res["camera"]), mvp.reshape(-1))
+    inv, seeds = capi.schedule(mvp, 1920, 1080, 3, 17)
+    assert _eq(np.array(res["scheduleInv"], np.float32), inv.reshape(-1)) and _eq(np.array(res["scheduleSeeds"], np.float32), seeds)
+    assert _eq(np.array(res["tiles"], np.int32), capi.partition_tiles(1920, 1080, 3, 8).reshape(-1))
+    assert len(res["rows"]) == 12
