@@ -25,7 +25,9 @@ SM_D double reduce_pio2(double x, int& q) {
   double r = x - k * kP1;
   r = r - k * kP2;
   r = r - k * kP3;
-  q = (int)((long long)k & 3);
+  // q = k mod 4 (two's complement, = (long long)k & 3): k is integral with |k| < 2^50, so k + 1.5*2^52 is exact
+  // and its low word holds k mod 2^32 (one f64 add instead of the compiler's 64-bit conversion sequence)
+  q = (int)(__double2loint(k + 6755399441055744.0) & 3);
   return r;
 }
 constexpr double kLn2Hi = 0.6931471803691238;

@@ -90,9 +90,23 @@ D V3 localToWorld(V3 v, V3 ns, V3 ss, V3 ts) {
   return v3(ss.x * v.x + ts.x * v.y + ns.x * v.z, ss.y * v.x + ts.y * v.y + ns.y * v.z,
             ss.z * v.x + ts.z * v.y + ns.z * v.z);
 }
-// OBJECT_SPACE_N/S/T (define.glsl:62-64); kept as full dot products so -0 / NaN propagate like the reference
+// OBJECT_SPACE_N/S/T (define.glsl:62-64): the full dot products of the reference, so -0 / NaN propagate the same.
+// A product with an exact 0 is exact (a signed zero, or NaN), so "a*0 + b" rounds once either way and is written
+// fma(a, 0, b): bit for bit the same sum (the zero-sum sign rule of fma is the addition's) in fewer instructions.
+#ifndef SAIL_AXIS_FMA
+#define SAIL_AXIS_FMA 1
+#endif
+#if SAIL_AXIS_FMA
+D V3 W2L(V3 v) {  // (dot(v, (0,0,-1)), dot(v, (1,0,0)), dot(v, (0,1,0)))
+  return v3(fma_(v.y, 0.0f, v.x * 0.0f) - v.z, fma_(v.z, 0.0f, fma_(v.y, 0.0f, v.x)), fma_(v.z, 0.0f, fma_(v.x, 0.0f, v.y)));
+}
+D V3 L2W(V3 v) {  // (0,0,-1) v.x + (1,0,0) v.y + (0,1,0) v.z, row by row as localToWorld sums them
+  return v3(fma_(v.z, 0.0f, fma_(v.x, 0.0f, v.y)), fma_(v.y, 0.0f, v.x * 0.0f) + v.z, fma_(v.z, 0.0f, fma_(v.y, 0.0f, -v.x)));
+}
+#else
 D V3 W2L(V3 v) { return worldToLocal(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
 D V3 L2W(V3 v) { return localToWorld(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
+#endif
 D bool equalZero(float x) { return x < 1e-3f && x > -1e-3f; }
 D float sgn(int rev) { return rev ? -1.0f : 1.0f; }
 
@@ -301,8 +315,14 @@ D V3 normalForCornellbox(V3 hit, const SailPrim& p) {  // cornellbox.glsl:39-51
   return v3(0.0f, 0.0f, 1.0f);
 }
 D void dpdBox(V3 normal, V3& dpdu, V3& dpdv) {
+#if SAIL_AXIS_FMA
+  const V3 n = normal;  // cross(n, (1,0,0)) / cross(n, (0,1,0)) with the exact zero products folded (see W2L)
+  if (fabsf(n.x) < 0.5f) dpdu = v3(fma_(n.y, 0.0f, n.z * -0.0f), fma_(n.x, -0.0f, n.z), fma_(n.x, 0.0f, -n.y));
+  else dpdu = v3(fma_(n.y, 0.0f, -n.z), fma_(n.z, 0.0f, n.x * -0.0f), fma_(n.y, -0.0f, n.x));
+#else
   if (fabsf(normal.x) < 0.5f) dpdu = cross(normal, v3(1.0f, 0.0f, 0.0f));
   else dpdu = cross(normal, v3(0.0f, 1.0f, 0.0f));
+#endif
   dpdv = cross(normal, dpdu);
 }
 D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
