@@ -385,6 +385,21 @@ D float phiOf(float y, float x) {
   return phi;
 }
 D V3 dpduRot(V3 hit) { return v3(-2.0f * kPI * hit.y, 2.0f * kPI * hit.x, 0.0f); }
+// cross(a, b) with a.z == 0 (crossZa) or b.z == 0 (crossZb), the exact zero products folded as in W2L
+D V3 crossZa(V3 a, V3 b) {
+#if SAIL_AXIS_FMA
+  return v3(fma_(b.y, -0.0f, a.y * b.z), fma_(b.x, 0.0f, -(a.x * b.z)), a.x * b.y - a.y * b.x);
+#else
+  return cross(a, b);
+#endif
+}
+D V3 crossZb(V3 a, V3 b) {
+#if SAIL_AXIS_FMA
+  return v3(fma_(a.y, 0.0f, -(a.z * b.y)), fma_(a.x, -0.0f, a.z * b.x), a.x * b.y - a.y * b.x);
+#else
+  return cross(a, b);
+#endif
+}
 D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const float rad = p.a[3];
   // theta of the UV and of computeDpDForSphere (:33-43) are the same value: the pole guard touches x only
@@ -401,7 +416,7 @@ D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const float cosPhi = hl.x * invZRadius, sinPhi = hl.y * invZRadius;
   const V3 dpdu = dpduRot(hl);
   const V3 dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(th2));
-  const V3 nl = normalize(cross(dpdv, dpdu));
+  const V3 nl = normalize(crossZb(dpdv, dpdu));  // dpdu.z == 0
   h.sc = getSurfaceColor(c, uv, p);
   h.hit = L2W(hl) + P3(p, 0);
   h.normal = L2W(nl);
@@ -560,8 +575,9 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
   return t;
 }
 // local-space tail shared by the quadrics and the disk: normal from dpdu x dpdv, texture, back to world
+// dpdu is dpduRot(hit) for every caller (z == 0)
 D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dpdv, Hit& h) {
-  const V3 nl = normalize(cross(dpdu, dpdv));
+  const V3 nl = normalize(crossZa(dpdu, dpdv));
   h.sc = getSurfaceColor(c, uv, p);
   h.hit = L2W(hl) + P3(p, 0);
   h.normal = L2W(nl);
@@ -1016,9 +1032,11 @@ D V3 frEvaluate(const Fr& f, float cosThetaI) {
 }
 D V3 trSampleWh(V2 u, float ax, float ay, V3 wo) {  // microfacet.glsl:41-59
   float cosT = 0.0f, phi = 2.0f * kPI * u.x;
+  float sp, cp;  // sin/cos of the final phi: the anisotropic branch has them already
   if (ax == ay) {
     const float tanTheta2 = fdiv(ax * ax * u.x, 1.0f - u.x);
     cosT = rcp_rn(sqrtf_(1.0f + tanTheta2));
+    sincosf_(phi, sp, cp);
   } else {
     phi = atanf_(fdiv(ay, ax) * tanf_(kPiOver2 + 2.0f * kPI * u.x));
     if (u.x > 0.5f) phi += kPI;
@@ -1027,9 +1045,9 @@ D V3 trSampleWh(V2 u, float ax, float ay, V3 wo) {  // microfacet.glsl:41-59
     const float alpha2 = rcp_rn(fdiv(cP * cP, ax2) + fdiv(sP * sP, ay2));
     const float tanTheta2 = fdiv(alpha2 * u.x, 1.0f - u.x);
     cosT = rcp_rn(sqrtf_(1.0f + tanTheta2));
+    sp = sP; cp = cP;
   }
   const float sinT = sqrtf_(fmax_(0.0f, 1.0f - cosT * cosT));
-  float sp, cp; sincosf_(phi, sp, cp);
   V3 wh = v3(sinT * cp, sinT * sp, cosT);
   if (!sameHemisphere(wo, wh)) wh = -wh;
   return wh;
