@@ -162,6 +162,23 @@ SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 SM_D float clamp_(float x, float lo, float hi) { return fmin_(fmax_(x, lo), hi); }
 SM_D float fract_(float x) { return x - floorf(x); }
 SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }
+// sqrtf_ for arguments that are +-0, NaN or in [2^-96, 1] by construction, where v_sqrt_f32 plus the
+// two-neighbour residual correction equals the IEEE square root bit for bit (tools/sqrt01_probe.hip: every such f32
+// on an MI355X; below 2^-96 the hardware root needs the general lowering's scaling). The callers' arguments:
+//  * max(0, 1 - t), 1 - t with t in [0, 1]: 0, or at least 2^-24 (1 - t is exact for t > 1/2, >= 1/2 otherwise);
+//  * fract(y) of the hash (random.glsl), y = RN(A + s), A = RN(sin(.) 43758.5453), s = RN(seed + depth): a nonzero
+//    y below 1 is a multiple of the smaller ulp of A and s; |s| is 0 or >= 2^-24 (seed near -depth has ulp >=
+//    2^-24), |A| is 0 or far above 2^-60 (the sine of an f32 argument of magnitude >= 75 stays above ~2^-30), so
+//    fract(y) is 0 or above 2^-84; y >= 1 leaves multiples of 2^-23.
+// The general lowering's scaling and class fix-ups (7 instructions) are not needed there.
+SM_D float sqrt01(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+  float r = s;
+  if (__builtin_fmaf(-sdn, s, x) <= 0.0f) r = sdn;
+  if (__builtin_fmaf(-sup, s, x) > 0.0f) r = sup;
+  return r;
+}
 // GLSL division a / b := a * RN(1/b) (the reciprocal-multiply form shader compilers emit, with the reciprocal
 // correctly rounded; oracle/ref_math.h div_s). RN(1/b) = one Newton step from the hardware reciprocal, equal to
 // the IEEE 1.0f / b for every f32 b with 2^-126 <= |b| <= 2^126 (all 2^32 inputs checked on an MI355X:

@@ -193,6 +193,15 @@ D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
 D float TP(const Ctx& c, int row, int col) { return constRow<float>(c.tp, row * 16 + col); }
 D V3 TP3(const Ctx& c, int row, int col) { return v3(TP(c, row, col), TP(c, row, col + 1), TP(c, row, col + 2)); }
 
+// the square root of the warps and BSDF terms whose argument is in [0, 1] by construction (sail_math.h sqrt01)
+#ifndef SAIL_SQRT01
+#define SAIL_SQRT01 1
+#endif
+#if SAIL_SQRT01
+#define SQRT01(x) sqrt01(x)
+#else
+#define SQRT01(x) sqrtf_(x)
+#endif
 // ---- random.glsl:5-18 ---------------------------------------------------------------------------------
 D float hash1(const Ctx& c, float seed, float a, float b, float cc) {
   const V3 p = v3(c.fcx + seed, c.fcy + seed, 0.5f + seed);
@@ -205,16 +214,16 @@ D V2 random2(const Ctx& c, float seed) {
 // ---- sampler.glsl ---------------------------------------------------------------------------------------
 D V3 uniformSampleSphere(V2 u) {
   const float z = 1.0f - 2.0f * u.x;
-  const float r = sqrtf_(1.0f - z * z);
+  const float r = SQRT01(1.0f - z * z);
   const float angle = 2.0f * kPI * u.y;
   float s, co; sincosf_(angle, s, co);
   return v3(r * co, r * s, z);
 }
 D V3 cosineSampleHemisphere(V2 u) {
-  const float r = sqrtf_(u.x);
+  const float r = SQRT01(u.x);
   const float angle = 2.0f * kPI * u.y;
   float s, co; sincosf_(angle, s, co);
-  return v3(r * co, r * s, sqrtf_(1.0f - u.x));
+  return v3(r * co, r * s, SQRT01(1.0f - u.x));
 }
 D V2 concentricSampleDisk(V2 u) {
   const float uOffset = 2.0f * u.x - 1.0f, vOffset = 2.0f * u.y - 1.0f;
@@ -985,7 +994,7 @@ D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
 // ---- ssutility.glsl / fresnel.glsl / microfacet.glsl / bsdf.glsl --------------------------------------------------
 D float absCosTheta(V3 w) { return fabsf(w.z); }
 D float sin2Theta(V3 w) { return fmax_(0.0f, 1.0f - w.z * w.z); }
-D float sinTheta(V3 w) { return sqrtf_(sin2Theta(w)); }
+D float sinTheta(V3 w) { return SQRT01(sin2Theta(w)); }
 D float tan2Theta(V3 w) {
   const float cos2T = w.z * w.z;
   if (cos2T < kEps) return kInf;
@@ -997,10 +1006,10 @@ D bool sameHemisphere(V3 w, V3 wp) { return w.z * wp.z > kEps; }
 
 D float frDielectric(float cosThetaI, float etaI, float etaT) {
   cosThetaI = clamp_(cosThetaI, -1.0f, 1.0f);
-  const float sinThetaI = sqrtf_(fmax_(0.0f, 1.0f - cosThetaI * cosThetaI));
+  const float sinThetaI = SQRT01(fmax_(0.0f, 1.0f - cosThetaI * cosThetaI));
   const float sinThetaT = fdiv(etaI, etaT) * sinThetaI;
   if (sinThetaT >= 1.0f) return 1.0f;
-  const float cosThetaT = sqrtf_(fmax_(0.0f, 1.0f - sinThetaT * sinThetaT));
+  const float cosThetaT = SQRT01(fmax_(0.0f, 1.0f - sinThetaT * sinThetaT));
   const float TI = etaT * cosThetaI, IT = etaI * cosThetaT, II = etaI * cosThetaI, TT = etaT * cosThetaT;
   const float Rparl = fdiv(TI - IT, TI + IT), Rperp = fdiv(II - TT, II + TT);
   return fdiv(Rparl * Rparl + Rperp * Rperp, 2.0f);
@@ -1047,7 +1056,7 @@ D V3 trSampleWh(V2 u, float ax, float ay, V3 wo) {  // microfacet.glsl:41-59
     cosT = rcp_rn(sqrtf_(1.0f + tanTheta2));
     sp = sP; cp = cP;
   }
-  const float sinT = sqrtf_(fmax_(0.0f, 1.0f - cosT * cosT));
+  const float sinT = SQRT01(fmax_(0.0f, 1.0f - cosT * cosT));
   V3 wh = v3(sinT * cp, sinT * sp, cosT);
   if (!sameHemisphere(wo, wh)) wh = -wh;
   return wh;
@@ -1903,6 +1912,7 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
     case 10: r = fmax_(x[i], y[i]); break;
     case 11: r = fdiv(x[i], y[i]); break;  // GLSL divide spec
     case 14: r = rcp_rn(x[i]); break;
+    case 15: r = sqrt01(x[i]); break;  // callers guarantee [0, 1] or NaN
     case 12: r = clamp_(x[i], 0.0f, 1.0f); break;
     default: break;
   }

@@ -76,6 +76,23 @@ def test_math_spec_bit_exact(gpu, fn):
     assert same.all(), f"fn {fn}: {int((~same).sum())} mismatches, e.g. x={x[~same][:3]} gpu={got[~same][:3]} cpu={want[~same][:3]}"
 
 
+def test_sqrt01_equals_ieee_sqrt_on_its_domain(gpu):
+    """sail_math.h sqrt01 (no scaling / class fix-ups) is used only where the argument is +-0, NaN or in [2^-96, 1]
+    (the argument bounds are in its header); there it must be the IEEE square root: every 1024th f32 of that range,
+    the 2^16 patterns nearest 2^-96 and 1, both zeros and NaN payloads (tools/sqrt01_probe.hip checks every one of
+    them on the GPU)"""
+    one, lo = int(np.float32(1.0).view(np.uint32)), int(np.float32(2.0 ** -96).view(np.uint32))
+    bits = np.concatenate([np.arange(lo, one + 1, 1024, dtype=np.uint64),
+                           np.arange(lo, lo + (1 << 16), dtype=np.uint64), np.array([0], np.uint64),
+                           np.arange(one - (1 << 16), one + 1, dtype=np.uint64),
+                           np.array([0x80000000, 0x7FC00000, 0xFFC00000, 0x7F800001, 0x7FFFFFFF], np.uint64)])
+    x = bits.astype(np.uint32).view(np.float32)
+    got = capi.math_probe(15, x, np.zeros_like(x))
+    want = oracle.math(7, x, np.zeros_like(x))
+    same = bit_equal(got, want)
+    assert same.all(), f"{int((~same).sum())} mismatches, e.g. bits {bits[~same][:4]}"
+
+
 # ---- trace parity ------------------------------------------------------------------------------------------
 CASES = [
     # scene, W, H, spp, bounces
