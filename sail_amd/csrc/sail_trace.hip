@@ -160,6 +160,7 @@ struct PhaseClock {};
 #endif
 struct Hit {
   float d; V3 hit, normal, dpdu, dpdv; bool into; int matRow; V3 sc, emission; int matCategory;
+  float nd;  // dot(geometric normal before the into flip, ray direction)
 };
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
@@ -888,10 +889,13 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   }
   h.matRow = p.matRow;
   h.emission = v3(p.em[0], p.em[1], p.em[2]);
-  const V3 nn = sgn(p.rev) * h.normal;                       // faceObj test (shader.shape.js:47-49)
-  if (!(dot(nn, r.d) < -kEps)) h.emission = v3s(0.0f);
+  // faceObj test (shader.shape.js:47-49) on sgn(rev) * normal: (-n).d is exactly -(n.d) (negated products,
+  // round-to-nearest is symmetric), so one dot product serves it and the into test below
+  const float nd = dot(h.normal, r.d);
+  if (!((p.rev ? -nd : nd) < -kEps)) h.emission = v3s(0.0f);
   h.matCategory = matCat(p);
-  h.into = dot(h.normal, r.d) < -kEps;
+  h.into = nd < -kEps;
+  h.nd = nd;
   if (!h.into) h.normal = -h.normal;
   return h;
 }
@@ -914,7 +918,7 @@ D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc)
     Hit h;
     h.d = sw.best;
     h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
-    h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0;
+    h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0; h.nd = 0.0f;
     return h;
   }
   return hitRecord(c, r, sw);
@@ -1292,7 +1296,10 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
 #else
     const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
 #endif
-    const V3 wo = worldToLocal(-ray.d, ins.normal, ss, ts);
+    // worldToLocal(-ray.d, normal, ss, ts): its z is dot(-d, +-n) = -+(n.d) exactly (negated products, symmetric
+    // rounding), already known from the hit record's into test
+    const V3 nd3 = -ray.d;
+    const V3 wo = v3(dot(nd3, ss), dot(nd3, ts), ins.into ? -ins.nd : ins.nd);
     // the hash is evaluated only for materials that consume it (matte/metal/glass; mirror is deterministic)
     PHASE_MARK(pc, 2);  // shading frame
     const V2 u2 = (ins.matCategory != SAIL_MIRROR) ? random2(c, seed) : v2(0.0f, 0.0f);
@@ -1303,7 +1310,12 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
     const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
     PHASE_MARK(pc, 4);  // BSDF sample
     V3 direct = v3s(0.0f);
-    if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) direct = direct + lightSample(c, ins, u2) * f;
+    if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) {
+      if (c.kLights == 0)  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
+        direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
+      else
+        direct = direct + lightSample(c, ins, u2) * f;
+    }
     PHASE_MARK(pc, 5);  // light sample + shadow ray
     const V3 sh = ins.emission + direct;
     e = e + sh * fpdf;
