@@ -159,7 +159,16 @@ SM_D float expf_(float x) { return (float)exp_d((double)x); }  // wavelet weight
 // GLSL min/max/clamp: the hardware v_min_f32/v_max_f32 (a NaN operand yields the other; -0 < +0)
 SM_D float fmin_(float a, float b) { return __builtin_fminf(a, b); }
 SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
-SM_D float clamp_(float x, float lo, float hi) { return fmin_(fmax_(x, lo), hi); }
+// clamp = max then min. With the bounds (0, 1) or (-1, 1) that is exactly one v_med3_f32 (which the compiler
+// may also fold into the producing instruction's output clamp modifier): equal for every f32 x, NaN and signed
+// zeros included (tools/med3_probe.hip, all 2^32 inputs on an MI355X, profiles/r02_med3_probe.json)
+SM_D float clamp_(float x, float lo, float hi) {
+#if !defined(SAIL_NO_MED3)
+  if (__builtin_constant_p(lo) && __builtin_constant_p(hi) && (lo == 0.0f || lo == -1.0f) && hi == 1.0f)
+    return __builtin_amdgcn_fmed3f(x, lo, hi);
+#endif
+  return fmin_(fmax_(x, lo), hi);
+}
 SM_D float fract_(float x) { return x - floorf(x); }
 SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }
 // sqrtf_ for arguments that are +-0, NaN or in [2^-96, 1] by construction, where v_sqrt_f32 plus the

@@ -76,7 +76,7 @@ D float length(V3 v) { return sqrtf_(dot(v, v)); }
 D V3 normalize(V3 v) { return v / length(v); }
 D V3 vmin(V3 a, V3 b) { return v3(fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)); }
 D V3 vmax(V3 a, V3 b) { return v3(fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)); }
-D V3 vclamp01(V3 x) { return vmin(vmax(x, v3s(0.0f)), v3s(1.0f)); }
+D V3 vclamp01(V3 x) { return v3(clamp_(x.x, 0.0f, 1.0f), clamp_(x.y, 0.0f, 1.0f), clamp_(x.z, 0.0f, 1.0f)); }
 D bool isBlack(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
 D V3 reflect_(V3 I, V3 N) { return I - (2.0f * dot(N, I)) * N; }
 D V3 refract_(V3 I, V3 N, float eta) {
@@ -1327,7 +1327,7 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
 }
 
 D float q8(float v) {
-  v = fmin_(fmax_(v, 0.0f), 1.0f);
+  v = clamp_(v, 0.0f, 1.0f);
   return floorf(v * 255.0f + 0.5f) / 255.0f;
 }
 // fstrace.glsl:13 accumulation of one sample (SUM: running sums + count; MIX / COMPAT8: the reference's
@@ -1880,7 +1880,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_filter_kernel(SailFilterA
   const size_t pix = (size_t)y * A.W + x;
   if (A.out) A.out[pix] = make_float4(o[0], o[1], o[2], o[3]);
   if (A.out8) {
-    for (int c = 0; c < 3; c++) A.out8[4 * pix + c] = (uint8_t)(int)(fmin_(fmax_(o[c], 0.0f), 1.0f) * 255.0f + 0.5f);
+    for (int c = 0; c < 3; c++) A.out8[4 * pix + c] = (uint8_t)(int)(clamp_(o[c], 0.0f, 1.0f) * 255.0f + 0.5f);
     A.out8[4 * pix + 3] = 255;
   }
 }
