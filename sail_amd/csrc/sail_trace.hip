@@ -1475,22 +1475,29 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
-template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
+// NT threads per workgroup (ungrouped kernels only; grouped ones keep 256): a 16 x NT/16 pixel block, 4096/NT
+// blocks per 64x64 tile. A larger workgroup sorts a larger pool of paths (fewer mixed waves) at the price of a
+// wider barrier.
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
+  static_assert(NT == 256 || ((NT == 512 || NT == 1024) && !GROUPED), "grouped kernels share the 256-thread stage layout");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
-  __shared__ float sSt[kFields][256];
-  __shared__ float sE[3][256];
+  __shared__ float sSt[kFields][NT];
+  __shared__ float sE[3][NT];
   __shared__ int sCnt[kKeys];
   __shared__ int sStart[kKeys + 1];
-  const TileWork tw = tileWork<GROUPED>(A);
+  TileWork tw = tileWork<GROUPED>(A);
+  if (NT != 256) {
+    tw.bid = (int)blockIdx.x; tw.ownedTile = tw.bid / (4096 / NT); tw.sub = tw.bid % (4096 / NT);
+  }
   const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
   const int sub = tw.sub;
   const int tile = A.rank + ownedTile * A.world;
   const int tx = tile % A.tilesX, ty = tile / A.tilesX;
   const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
-  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * 16;
+  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * (NT / 16);
   const int x = x0 + (li & 15), y = y0 + (li >> 4);
   const bool valid = x < A.W && y < A.H;   // ragged tiles: invalid lanes still serve migrated paths
 
@@ -1649,6 +1656,13 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 
 // each plugin set has an ungrouped kernel (one workgroup per 16x16 block, every sample) and a _grouped one
 // (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel)
+#define SAIL_TRACE_KERNELS_NT(name, waves, body, cull, ks, km, kt, kl, nt)                                       \
+  extern "C" __global__ void __launch_bounds__(nt, waves) name(SailTraceArgs A) {                                \
+    body<cull, false, ks, km, kt, kl, nt>(A);                                                                    \
+  }                                                                                                              \
+  extern "C" __global__ void __launch_bounds__(256, waves) name##_grouped(SailTraceArgs A) {                     \
+    body<cull, true, ks, km, kt, kl>(A);                                                                         \
+  }
 #define SAIL_TRACE_KERNELS(name, waves, body, cull, ks, km, kt, kl)                                              \
   extern "C" __global__ void __launch_bounds__(256, waves) name(SailTraceArgs A) {                               \
     body<cull, false, ks, km, kt, kl>(A);                                                                        \
@@ -1668,8 +1682,12 @@ SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, SAIL_GENERIC_TILE, f
 #ifndef SAIL_CORNELL_CULL
 #define SAIL_CORNELL_CULL false
 #endif
-SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
-                   SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS)
+#ifndef SAIL_CORNELL_NT
+#define SAIL_CORNELL_NT 256
+#endif
+SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
+                      SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS,
+                      SAIL_CORNELL_NT)
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
 #ifndef SAIL_TRACE_ROOM_MIN_WAVES
 #define SAIL_TRACE_ROOM_MIN_WAVES 7
@@ -1680,8 +1698,11 @@ SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL
 #ifndef SAIL_ROOM_CULL
 #define SAIL_ROOM_CULL false
 #endif
-SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
-                   SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS)
+#ifndef SAIL_ROOM_NT
+#define SAIL_ROOM_NT 256
+#endif
+SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
+                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT)
 // the pre-cull kernel serves scenes with many primitives (C4: 7 waves measured best of 5-8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
@@ -1689,7 +1710,11 @@ SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_
 #ifndef SAIL_CULL_TILE
 #define SAIL_CULL_TILE SAIL_TILE_SMALL
 #endif
-SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u)
+// threads per workgroup of the ungrouped pre-cull kernel (sail_launch_trace sizes its grid to match)
+#ifndef SAIL_CULL_NT
+#define SAIL_CULL_NT 1024
+#endif
+SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT)
 
 // ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
 extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {
@@ -1947,11 +1972,18 @@ extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) {
   const bool g = A.sampleGroups > 1;
 #define SAIL_LAUNCH(k) hipLaunchKernelGGL(g ? k##_grouped : k, dim3(blocks), dim3(256), 0, s, A)
-  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH(sail_trace_kernel_cornell);
-  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH(sail_trace_kernel_room);
-  else if (A.cullPrims) SAIL_LAUNCH(sail_trace_kernel_cull);
+  // ungrouped launches of an NT-thread kernel: blocks = ownedTiles * 16 of 256 threads -> ownedTiles * 4096 / NT
+#define SAIL_LAUNCH_NT(k, nt)                                                                   \
+  do {                                                                                          \
+    if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks), dim3(256), 0, s, A);                   \
+    else hipLaunchKernelGGL(k, dim3(blocks / ((nt) / 256)), dim3(nt), 0, s, A);                 \
+  } while (0)
+  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT);
+  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT);
+  else if (A.cullPrims) SAIL_LAUNCH_NT(sail_trace_kernel_cull, SAIL_CULL_NT);
   else SAIL_LAUNCH(sail_trace_kernel);
 #undef SAIL_LAUNCH
+#undef SAIL_LAUNCH_NT
   return hipGetLastError();
 }
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s) {

@@ -359,7 +359,7 @@ def test_kernel_selection(gpu, fixtures):
 
 
 # ---- sample groups (small per-rank frames): staged samples added in order are bit-identical ---------------------
-@pytest.mark.parametrize("name", ["C1", "C3"])
+@pytest.mark.parametrize("name", ["C1", "C3", "C4"])   # C4: the pre-cull kernel, 1024 threads when ungrouped
 @pytest.mark.parametrize("groups", ["1", "2", "5"])
 @pytest.mark.parametrize("mode", [capi.ACCUM_SUM, capi.ACCUM_MIX])
 def test_sample_groups(gpu, fixtures, monkeypatch, name, groups, mode):
@@ -489,6 +489,18 @@ def test_coverage_scenes_bit_exact(gpu, fixtures, monkeypatch, name, W, H, spp, 
         assert fin.all()
     if name == "N0":
         assert (want[..., :3] == 0).all() and segs == W * H * spp
+
+
+@pytest.mark.parametrize("name", ["AREA0", "ALL", "BILERP", "N1"])
+def test_cull_kernel_ungrouped_small_frames(gpu, fixtures, monkeypatch, name):
+    """The ungrouped pre-cull kernel runs 1024-thread workgroups (16 x 64 pixel strips, sail_trace.hip SAIL_CULL_NT):
+    forced on for small scenes and ragged frames (sample groups off), it must stay bit-exact"""
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, 0)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_SAMPLE_GROUPS, 1)
+    got, want, st, segs, gaov, waov = _render_both(fixtures, name, 70, 83, 3, 6, aov=True, launch=2)
+    assert bit_equal(got, want).all()
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
 
 
 def test_coverage_kernel_selection(gpu, fixtures):
