@@ -1,9 +1,10 @@
 // oracle/ref_math.h — TEST INFRASTRUCTURE (CPU oracle only; never linked into the product).
 //
-// Bit-defined fp32 transcendentals ("compat" math spec v2, SURVEY §7 hard parts: RNG parity).
+// Bit-defined fp32 transcendentals ("compat" math spec v3, SURVEY §7 hard parts: RNG parity).
 // GLSL leaves sin/cos/atan/acos/pow precision to the vendor (random.glsl:1-18 evaluates sin at
 // arguments of 1e4..1e6, where a 1-ulp difference yields an unrelated sample), so the build DEFINES
-// each one as a fixed sequence of IEEE-754 operations: f64 range reduction for sin/cos/tan, then f32
+// each one as a fixed sequence of IEEE-754 operations: range reduction for sin/cos/tan (three f32 FMAs below 2^20,
+// exact f64 beyond), then f32
 // polynomials with explicit fused multiply-adds (fmaf); no contraction anywhere else, no libm.
 // The HIP kernel implements the same spec independently in sail_amd/csrc/sail_math.h; the GPU parity
 // tests check the two bit-for-bit over millions of arguments.
@@ -100,7 +101,7 @@ static inline double log_d(double x) {
   return ((double)e * kLn2Hi + (2.0 * s) * p) + (double)e * kLn2Lo;
 }
 
-// ---- the f32 spec functions (spec v2) ------------------------------------------------------------------
+// ---- the f32 spec functions (spec v3) ------------------------------------------------------------------
 // sin/cos/tan: the f64 Cody-Waite reduction above (exact k*P_i for |x| < ~1.6e6, which covers the hash
 // RNG's 1e4..1e6 arguments), then ONE rounding of r to f32 and f32 polynomials evaluated with fused
 // multiply-adds (fmaf: correctly rounded on every platform). atan/atan2/acos are f32 throughout.
@@ -124,9 +125,23 @@ static inline float cospoly_f(float r) {  // 1 - r^2/2 + r^4 Q(r^2)
   const float q = fmaf(fmaf(kC2, z, kC1), z, kC0);
   return fmaf(z * z, q, fmaf(-0.5f, z, 1.0f));
 }
+// spec v3 reduction (sail_math.h reduce_spec): |x| < 2^20 -> j = rint(RN(x * 2/pi)) (round half to even), then
+// r = x - j*(A + B + C) by three FMAs; beyond, the f64 reduction above rounded to f32
+static const float kInvPiO2F = 0x1.45f306p-1f, kPiO2A = 0x1.921fb6p+0f, kPiO2B = -0x1.777a5cp-25f,
+                   kPiO2C = -0x1.ee59dap-50f;
+static inline float reduce_spec(float x, int* q) {
+  if (fabsf(x) < 0x1p20f) {
+    const float j = rintf(x * kInvPiO2F);   // default rounding mode: to nearest, ties to even
+    float r = fmaf(-j, kPiO2A, x);
+    r = fmaf(-j, kPiO2B, r);
+    r = fmaf(-j, kPiO2C, r);
+    *q = (int)j & 3;
+    return r;
+  }
+  return (float)reduce_pio2((double)x, q);
+}
 static inline void sincos_s(float x, float* so, float* co) {
-  int q; const double r = reduce_pio2((double)x, &q);
-  const float rf = (float)r;
+  int q; const float rf = reduce_spec(x, &q);
   const float s = sinpoly_f(rf), c = cospoly_f(rf);
   switch (q) {
     case 0: *so = s; *co = c; break;
@@ -138,8 +153,7 @@ static inline void sincos_s(float x, float* so, float* co) {
 static inline float sin_s(float x) { float s, c; sincos_s(x, &s, &c); return s; }
 static inline float cos_s(float x) { float s, c; sincos_s(x, &s, &c); return c; }
 static inline float tan_s(float x) {
-  int q; const double r = reduce_pio2((double)x, &q);
-  const float rf = (float)r;
+  int q; const float rf = reduce_spec(x, &q);
   const float s = sinpoly_f(rf), c = cospoly_f(rf);
   return (q & 1) ? (-c / s) : (s / c);
 }

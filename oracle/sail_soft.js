@@ -42,7 +42,7 @@ function fma32(a, b, c) {
   return err > 0 ? hi : lo;
 }
 
-// ---- compat math spec v2 (oracle/ref_math.h) --------------------------------------------------------------
+// ---- compat math spec v3 (oracle/ref_math.h) --------------------------------------------------------------
 const kTwoOverPi = 0.6366197723675814, kP1 = 1.5707963267341256, kP2 = 6.077100506303966e-11,
   kP3 = 2.0222662487959506e-21;
 function reducePio2(x) {  // -> [r (f64), q]
@@ -63,9 +63,30 @@ const kB = [0.16666673123836517, 0.07498858869075775, 0.045000601559877396, 0.02
 const kPiF = f(3.14159274), kPiO2F = f(1.57079637);
 function sinpoly(r) { const z = f(r * r); return fma32(f(r * z), fma32(fma32(kS2, z, kS1), z, kS0), r); }
 function cospoly(r) { const z = f(r * r); return fma32(f(z * z), fma32(fma32(kC2, z, kC1), z, kC0), fma32(f(-0.5), z, 1)); }
-function sincos(x) {
+// spec v3 reduction (oracle/ref_math.h reduce_spec): |x| < 2^20 -> j = rint(RN(x * 2/pi)), ties to even, then three
+// exactly rounded f32 FMAs; beyond, the f64 reduction rounded to f32. -> [rf (f32), q]
+const kInvPiO2F = f(0.6366197466850281), kPiO2A = f(1.5707963705062866), kPiO2B = f(-4.371138828673793e-08),
+  kPiO2C = f(-1.7151245100058819e-15);
+function rintEven(v) {  // v: an f32 value; exact (v - floor(v) is exact below 2^52)
+  const n = Math.floor(v), d = v - n;
+  if (d > 0.5) return n + 1;
+  if (d < 0.5) return n;
+  return (n % 2 === 0) ? n : n + 1;
+}
+function reduceSpec(x) {
+  if (Math.abs(x) < 1048576) {
+    const j = rintEven(f(x * kInvPiO2F)), mj = -j;
+    let r = fma32(mj, kPiO2A, x);
+    r = fma32(mj, kPiO2B, r);
+    r = fma32(mj, kPiO2C, r);
+    return [r, ((j % 4) + 4) % 4];
+  }
   const [r, q] = reducePio2(x);
-  const rf = f(r), s = sinpoly(rf), c = cospoly(rf);
+  return [f(r), q];
+}
+function sincos(x) {
+  const [rf, q] = reduceSpec(x);
+  const s = sinpoly(rf), c = cospoly(rf);
   switch (q) {
     case 0: return [s, c];
     case 1: return [c, -s];
@@ -76,8 +97,8 @@ function sincos(x) {
 function sin_(x) { return sincos(x)[0]; }
 function cos_(x) { return sincos(x)[1]; }
 function tan_(x) {
-  const [r, q] = reducePio2(x);
-  const rf = f(r), s = sinpoly(rf), c = cospoly(rf);
+  const [rf, q] = reduceSpec(x);
+  const s = sinpoly(rf), c = cospoly(rf);
   return (q & 1) ? f(-c / s) : f(s / c);
 }
 function atan01(t) {

@@ -1,10 +1,10 @@
-// sail_math.h — device implementation of the build's bit-defined f32 math spec v2 ("compat" RNG mode).
+// sail_math.h — device implementation of the build's bit-defined f32 math spec v3 ("compat" RNG mode).
 //
 // GLSL leaves sin/cos/atan/acos/pow accuracy to the vendor, and Sail's hash RNG
 // (src/shader/util/random.glsl:1-18) evaluates sin() at 1e4..1e6 where one ulp decides the sample, so
-// the build defines each transcendental as a fixed IEEE operation sequence: an exact f64 Cody-Waite
-// reduction for sin/cos/tan (the only f64 work: ~8 ops), then f32 polynomials with explicit FMAs
-// (<= 2 ulp). The library is compiled with -ffp-contract=off, so no other FMA is formed. The CPU oracle
+// the build defines each transcendental as a fixed IEEE operation sequence: a Cody-Waite reduction for
+// sin/cos/tan (three f32 FMAs below 2^20, exact f64 beyond: reduce_spec), then f32 polynomials with explicit FMAs
+// (bounds in DESIGN.md §4). The library is compiled with -ffp-contract=off, so no other FMA is formed. The CPU oracle
 // carries an independent copy of the spec (oracle/ref_math.h); the GPU tests check them bit-for-bit.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -84,7 +84,7 @@ SM_D double log_d(double x) {
   return ((double)e * kLn2Hi + (2.0 * s) * p) + (double)e * kLn2Lo;
 }
 
-// ---- f32 spec functions (spec v2): f64 reduction for sin/cos/tan, then f32 polynomials with explicit
+// ---- f32 spec functions (spec v3): f32 / f64 reduction for sin/cos/tan (reduce_spec), then f32 polynomials with explicit
 //      fused multiply-adds (v_fma_f32 is correctly rounded: identical to the oracle's fmaf) ----
 constexpr float kS0 = -0.166666641831398f, kS1 = 0.008332744240760803f, kS2 = -0.0001958730281330645f;
 constexpr float kC0 = 0.0416666641831398f, kC1 = -0.0013888344401493669f, kC2 = 2.455315006955061e-05f;
@@ -104,9 +104,25 @@ SM_D float cospoly_f(float r) {
   const float z = r * r;
   return fma_(z * z, fma_(fma_(kC2, z, kC1), z, kC0), fma_(-0.5f, z, 1.0f));
 }
+// spec v3 reduction: for |x| < 2^20 (every hash argument of a frame up to ~60,000 samples, and every angle) the
+// f32 Cody-Waite reduction GPU libraries use: j = rint(RN(x * 2/pi)), r = x - j*(A + B + C) by three FMAs (A + B + C =
+// pi/2 to 2^-76; the first FMA is exact, each later one rounds once). Within 2.5 ulp of sin/cos for |x| < 1e4 and
+// within 2^-22 absolutely below 2^20 (tests/test_oracle_fixtures.py); beyond 2^20, the exact f64 reduction of v2.
+constexpr float kInvPiO2F = 0x1.45f306p-1f, kPiO2A = 0x1.921fb6p+0f, kPiO2B = -0x1.777a5cp-25f,
+                kPiO2C = -0x1.ee59dap-50f;
+SM_D float reduce_spec(float x, int& q) {
+  if (__builtin_expect(__builtin_fabsf(x) < 0x1p20f, 1)) {
+    const float j = __builtin_rintf(x * kInvPiO2F);
+    float r = fma_(-j, kPiO2A, x);
+    r = fma_(-j, kPiO2B, r);
+    r = fma_(-j, kPiO2C, r);
+    q = (int)j & 3;
+    return r;
+  }
+  return (float)reduce_pio2((double)x, q);
+}
 SM_D void sincosf_(float x, float& so, float& co) {
-  int q; const double r = reduce_pio2((double)x, q);
-  const float rf = (float)r;
+  int q; const float rf = reduce_spec(x, q);
   const float s = sinpoly_f(rf), c = cospoly_f(rf);
   so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
   co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
@@ -114,8 +130,7 @@ SM_D void sincosf_(float x, float& so, float& co) {
 SM_D float sinf_(float x) { float s, c; sincosf_(x, s, c); return s; }
 SM_D float cosf_(float x) { float s, c; sincosf_(x, s, c); return c; }
 SM_D float tanf_(float x) {
-  int q; const double r = reduce_pio2((double)x, q);
-  const float rf = (float)r;
+  int q; const float rf = reduce_spec(x, q);
   const float s = sinpoly_f(rf), c = cospoly_f(rf);
   return (q & 1) ? (-c / s) : (s / c);
 }

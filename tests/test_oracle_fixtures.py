@@ -166,11 +166,18 @@ def test_trowbridge_reitz_is_normalised():
 
 
 # ---- the spec transcendentals are accurate (they define, not approximate, the reference's vendor sin) ---------
-@pytest.mark.parametrize("fn,ref,lo,hi", [(0, np.sin, -1e6, 1e6), (0, np.sin, -7, 7), (1, np.cos, -1e6, 1e6),
-                                           (1, np.cos, -7, 7), (2, np.tan, -1.5, 1.5), (6, np.arctan, -1e3, 1e3),
-                                           (4, np.arccos, -1, 1), (3, None, 0, 0)])
-def test_spec_math_accuracy(fn, ref, lo, hi):
-    """spec v2 (f64 reduction + f32 FMA polynomials) stays within 2 ulp of the exact value"""
+# spec v3 (ref_math.h): sin/cos/tan reduce |x| < 2^20 in f32 (three FMAs, the GPU-library Cody-Waite form) and
+# beyond in exact f64; f32 FMA polynomials. Bounds: ulp of the exact value, or an absolute error ("abs") where the
+# f32 reduction's absolute accuracy is the statement (GLSL ES leaves transcendental precision to the vendor; the
+# Vulkan/ES highp bound for sin/cos is 2^-11 absolute inside [-pi, pi])
+@pytest.mark.parametrize("fn,ref,lo,hi,tol", [
+    (0, np.sin, -7, 7, 2.0), (0, np.sin, -1e4, 1e4, 3.0), (0, np.sin, -1e6, 1e6, ("abs", 2.0 ** -22)),
+    (0, np.sin, 1.05e6, 1.6e6, 2.0), (1, np.cos, -7, 7, 2.0), (1, np.cos, -1e4, 1e4, 3.0),
+    (1, np.cos, -1e6, 1e6, ("abs", 2.0 ** -22)), (1, np.cos, -1.6e6, -1.05e6, 2.0), (2, np.tan, -1.5, 1.5, 4.0),
+    (6, np.arctan, -1e3, 1e3, 2.0), (4, np.arccos, -1, 1, 2.0), (3, None, 0, 0, 2.0)])
+def test_spec_math_accuracy(fn, ref, lo, hi, tol):
+    """spec v3 stays within the stated bound of the exact value (tan = sin/cos adds one rounding, amplified near
+    pi/2)"""
     rng = np.random.default_rng(fn)
     if fn == 3:
         y = (rng.normal(size=50000) * 10 ** rng.uniform(-3, 3, 50000)).astype(np.float32)
@@ -181,9 +188,11 @@ def test_spec_math_accuracy(fn, ref, lo, hi):
         x = rng.uniform(lo, hi, 50000).astype(np.float32)
         got = oracle.math(fn, x).astype(np.float64)
         want = ref(x.astype(np.float64))
-    ulp = np.spacing(np.abs(want).astype(np.float32)).astype(np.float64)
-    tol = 4.0 if fn == 2 else 2.0  # tan = sin/cos adds one rounding and amplifies near pi/2
-    assert (np.abs(got - want) <= tol * ulp).all()
+    if isinstance(tol, tuple):
+        assert np.abs(got - want).max() <= tol[1]
+    else:
+        ulp = np.spacing(np.abs(want).astype(np.float32)).astype(np.float64)
+        assert (np.abs(got - want) <= tol * ulp).all()
 
 
 def test_division_spec_within_glsl_bound():

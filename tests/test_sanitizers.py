@@ -35,7 +35,12 @@ def _env():
         pytest.skip("clang ASan runtime / hipcc not available")
     if os.environ.get("LD_PRELOAD"):
         pytest.skip("another preload is active; the ASan runtime must load first")
-    if not os.path.exists(os.path.join(OUT, "libsail_hip_asan.so")) or not os.path.exists(os.path.join(OUT, "libsail_oracle_asan.so")):
+    libs = [os.path.join(OUT, "libsail_hip_asan.so"), os.path.join(OUT, "libsail_oracle_asan.so")]
+    srcs = [os.path.join(ROOT, d, f) for d in ("oracle", os.path.join("sail_amd", "csrc")) for f in os.listdir(os.path.join(ROOT, d))
+            if f.endswith((".cpp", ".h", ".hip", ".cc"))]
+    stale = not all(os.path.exists(p) for p in libs) or \
+        max(os.path.getmtime(p) for p in srcs) > min(os.path.getmtime(p) for p in libs)
+    if stale:  # missing, or older than the sources they instrument
         subprocess.run(["sh", os.path.join(ROOT, "tools", "sanitize_build.sh")], check=True, capture_output=True, timeout=900)
     env = dict(os.environ, LD_PRELOAD=rt,
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0",
