@@ -746,12 +746,46 @@ D bool padHitF(const SailPrim& p, const CullRay& q, float B) {
   const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
   return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > B);
 }
+// Mask build with the row's outcome as the compare's own lane mask (SAIL_MASK_ASM, fused form only): the bit is
+// shifted in by one v_addc (v + v + carry, the carry-in being that lane mask) instead of a select and a v_lshl_or,
+// and min(tmax, B) is one v_min_f32 -- the compiler's own fold of the three tests, which re-canonicalised the
+// loop-invariant B on every row (tmax and B are arithmetic results, never signalling NaNs, so the plain hardware
+// min is the same value). Two fewer VALU per row of the ~20 of each pre-cull test.
+#ifndef SAIL_MASK_ASM
+#define SAIL_MASK_ASM 1
+#endif
+#if SAIL_MASK_ASM
+D unsigned long long padHitFMask(const SailPrim& p, const CullRay& q, float B) {
+  const float x0 = fma_(p.a[18], q.rx, q.ox), x1 = fma_(p.a[21], q.rx, q.ox);
+  const float y0 = fma_(p.a[19], q.ry, q.oy), y1 = fma_(p.a[22], q.ry, q.oy);
+  const float z0 = fma_(p.a[20], q.rz, q.oz), z1 = fma_(p.a[23], q.rz, q.oz);
+  const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
+  const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
+  float mB;
+  __asm__("v_min_f32 %0, %1, %2" : "=v"(mB) : "v"(tmax), "v"(B));
+  // !(tmin > tmax) && !(tmin > B) == !(tmin > min(tmax, B)): a NaN tmax leaves B on either side
+  return __builtin_amdgcn_ballot_w64(!(tmin > mB)) & __builtin_amdgcn_ballot_w64(!(tmax < 0.0f));
+}
+D unsigned shiftInMask(unsigned v, unsigned long long laneMask) {
+  unsigned r;
+  unsigned long long carryOut;
+  __asm__("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carryOut) : "v"(v), "s"(laneMask));
+  return r;
+}
+#endif
 // one 64-row chunk's candidate mask: descending rows shifted into two 32-bit halves (one select and one
-// v_lshl_or per row)
+// v_lshl_or per row; one v_addc with SAIL_MASK_ASM)
 template <bool FUSED>
 D unsigned long long chunkMask(const Ctx& c, const Ray& r, const CullRay& q, int base, int cnt, float bound) {
   unsigned lo = 0u, hi = 0u;
   const float B = bound * 1.0001f + 1e-4f;
+#if SAIL_MASK_ASM
+  if (FUSED) {
+    for (int j = cnt - 1; j >= 32; j--) hi = shiftInMask(hi, padHitFMask(PRIM(c, base + j), q, B));
+    for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = shiftInMask(lo, padHitFMask(PRIM(c, base + j), q, B));
+    return ((unsigned long long)hi << 32) | lo;
+  }
+#endif
 #define SWEEP_TEST(j) (FUSED ? padHitF(PRIM(c, base + (j)), q, B) : CULL_TEST(c, PRIM(c, base + (j)), r, bound))
   for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (SWEEP_TEST(j) ? 1u : 0u);
   for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = (lo << 1) | (SWEEP_TEST(j) ? 1u : 0u);
