@@ -720,6 +720,11 @@ D void cullStat(bool pass) {
 #ifndef SAIL_CAND_RECULL
 #define SAIL_CAND_RECULL 0
 #endif
+// SAIL_CAND_FLAT=1: candidate loops without exec-mask nesting (idle lanes test a real row of the type, `take`
+// keeps them out): bit-identical, C4 -0.8 % (the idle lanes' own branches cost more than the saved masking)
+#ifndef SAIL_CAND_FLAT
+#define SAIL_CAND_FLAT 0
+#endif
 // candidate masks built from descending rows shifted into two 32-bit halves (one select + one v_lshl_or per
 // row instead of a 64-bit shift, two moves, two selects and two ors): C4 +2.7 %. Packing the x/y slab
 // arithmetic of padHit into v_pk_add_f32 / v_pk_mul_f32 (SAIL_CULL_PK) was measured at -3.4 %.
@@ -807,7 +812,27 @@ template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
 template <int T>
 D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
   if (!HAS(c.kShapes, T)) return;
-  unsigned long long m = cand & constRow<unsigned long long>(c.typeMasks, (base >> 6) * 16 + T);
+  const unsigned long long tm = constRow<unsigned long long>(c.typeMasks, (base >> 6) * 16 + T);
+  unsigned long long m = cand & tm;
+#if SAIL_CAND_FLAT
+  // every lane of the wave runs each iteration: a lane whose candidates of this type are used up tests the
+  // chunk's first row of type T (a real primitive of the same shape, so its branches stay those of a typical
+  // lane) and keeps its result out by `take`. No exec-mask nesting around the test, so the loop-carried winner
+  // needs no copies at every iteration.
+  while (__builtin_amdgcn_ballot_w64(m != 0ull)) {
+    const bool has = m != 0ull;
+    const int i = base + __builtin_ctzll(has ? m : tm);
+    m &= m - 1ull;  // 0 stays 0
+    const SailPrim& p = PRIM(c, i);
+    V3 hl = v3s(0.0f);
+    const float t = typedT<T>(p, r, &hl);
+    const bool take = has & ((t < best) | ((t == best) & (i < bi)));
+    best = take ? t : best;
+    bi = take ? i : bi;
+    bhl.x = take ? hl.x : bhl.x; bhl.y = take ? hl.y : bhl.y; bhl.z = take ? hl.z : bhl.z;
+  }
+  return;
+#endif
   while (__ballot(m != 0ull)) {
     if (m != 0ull) {
       const int i = base + __builtin_ctzll(m);
