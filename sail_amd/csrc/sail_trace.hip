@@ -93,10 +93,10 @@ D V3 localToWorld(V3 v, V3 ns, V3 ss, V3 ts) {
 // Box faces (Cube, Cornellbox): normal, dpdu, dpdv, ss and ts all have components in {0, +-1}, so every product of
 // their dot products, cross products and frame changes is exact, and each a*b + c rounds once: written fma(a, b, c),
 // bit for bit the unfused sum (the zero-sum sign rule of fma is the addition's; 0 * inf / NaN is NaN either way).
-// Measured bit-identical with ~20 fewer VALU per box-face bounce, yet C2 -1.2 %, C3 -0.8 %, C4 +0.8 % (the second
-// shading-frame branch costs more than it saves), so it is off by default.
+// Measured bit-identical with ~20 fewer VALU per box-face bounce: C2 -1.2 %, C3 -0.8 % (the second shading-frame
+// branch costs more than it saves there), C4 +0.9 %. 1 = every kernel, 2 (default) = the pre-cull kernel only.
 #ifndef SAIL_AXIS_FRAME
-#define SAIL_AXIS_FRAME 0
+#define SAIL_AXIS_FRAME 2
 #endif
 D float dotX(V3 a, V3 b) { return fma_(a.z, b.z, fma_(a.y, b.y, a.x * b.x)); }
 D V3 crossX(V3 a, V3 b) {
@@ -350,7 +350,7 @@ D void dpdBox(V3 normal, V3& dpdu, V3& dpdv) {
   if (fabsf(normal.x) < 0.5f) dpdu = cross(normal, v3(1.0f, 0.0f, 0.0f));
   else dpdu = cross(normal, v3(0.0f, 1.0f, 0.0f));
 #endif
-#if SAIL_AXIS_FRAME
+#if SAIL_AXIS_FRAME == 1
   dpdv = crossX(normal, dpdu);
 #else
   dpdv = cross(normal, dpdu);
@@ -1008,7 +1008,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // faceObj test (shader.shape.js:47-49) on sgn(rev) * normal: (-n).d is exactly -(n.d) (negated products,
   // round-to-nearest is symmetric), so one dot product serves it and the into test below
 #if SAIL_AXIS_FRAME
-  h.axis = p.type == SAIL_CUBE || p.type == SAIL_CORNELLBOX;
+  h.axis = (SAIL_AXIS_FRAME == 1 || c.cullPrims) && (p.type == SAIL_CUBE || p.type == SAIL_CORNELLBOX);
   const float nd = h.axis ? dotX(h.normal, r.d) : dot(h.normal, r.d);
 #else
   const float nd = dot(h.normal, r.d);
