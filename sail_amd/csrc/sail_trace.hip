@@ -866,7 +866,14 @@ template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
   else if constexpr (T == SAIL_CORNELLBOX) return cornellT(p, r);
   else return kMaxDistance;
 }
-template <int T>
+// HIT = false (shadow rays): only the closest distance is read, so neither the winner's row nor its local hit point
+// is kept, and an equally near candidate changes nothing (a tie leaves the distance's value as it is; +-0 compare
+// equal and both fail the caller's d > EPSILON). Four fewer live registers in the shadow sweep, where the
+// shading state is live.
+#ifndef SAIL_SHADOW_T_ONLY
+#define SAIL_SHADOW_T_ONLY 1
+#endif
+template <int T, bool HIT>
 D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
   if (!HAS(c.kShapes, T)) return;
   const unsigned long long tm = constRow<unsigned long long>(c.typeMasks, (base >> 6) * 16 + T);
@@ -898,13 +905,19 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
 #if SAIL_CAND_RECULL
       if (!padHit(p, r, best)) continue;
 #endif
-      V3 hl = v3s(0.0f);
-      const float t = typedT<T>(p, r, &hl);
-      if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
+      if (HIT || !SAIL_SHADOW_T_ONLY) {
+        V3 hl = v3s(0.0f);
+        const float t = typedT<T>(p, r, &hl);
+        if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
+      } else {
+        const float t = typedT<T>(p, r, nullptr);
+        if (t < best) best = t;
+      }
     }
   }
 }
 // limit: the pre-cull distance bound before any hit (kMaxDistance, or 1 for shadow rays: see closestT)
+template <bool HIT>
 D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, V3& bhl) {
   const CullRay q = cullRay(r);
   for (int base = 0; base < c.n; base += 64) {
@@ -912,15 +925,15 @@ D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, 
     const float bound = fmin_(best, limit);
     const unsigned long long cand =
         c.cullFma ? chunkMask<true>(c, r, q, base, cnt, bound) : chunkMask<false>(c, r, q, base, cnt, bound);
-    candType<SAIL_CUBE>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_CORNELLBOX>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_RECTANGLE>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_DISK>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_SPHERE>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_CYLINDER>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_CONE>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_PARABOLOID>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_HYPERBOLOID>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CUBE, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CORNELLBOX, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_RECTANGLE, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_DISK, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_SPHERE, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CYLINDER, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_CONE, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_PARABOLOID, HIT>(c, r, base, cand, best, bi, bhl);
+    candType<SAIL_HYPERBOLOID, HIT>(c, r, base, cand, best, bi, bhl);
   }
 }
 
@@ -933,7 +946,7 @@ D float closestT(const Ctx& c, const Ray& r) {
 #if SAIL_CAND_SWEEP
   if (c.cullPrims && !c.shadowAnyHit) {
     int bi = -1; V3 bhl = v3s(0.0f);
-    candSweep(c, r, 1.0f, best, bi, bhl);
+    candSweep<false>(c, r, 1.0f, best, bi, bhl);
     return best;
   }
 #endif
@@ -959,7 +972,7 @@ D Sweep sweepRay(const Ctx& c, const Ray& r, bool primary) {
   const bool cull = c.cullPrims && (!primary || c.cullPrimary);
 #if SAIL_CAND_SWEEP
   if (cull) {
-    candSweep(c, r, kMaxDistance, best, bi, bhl);
+    candSweep<true>(c, r, kMaxDistance, best, bi, bhl);
     Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
     return sw;
   }
@@ -1331,14 +1344,19 @@ D bool testShadow(const Ctx& c, const Ray& r) {
 // shadow sweep itself (the expensive part) is shared, so a wave whose lanes picked different light kinds
 // runs one sweep instead of one per kind. Contribution and visibility are independent pure functions of the
 // same inputs, so evaluating the contribution first changes no bit.
-D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
+// lightPrep: everything of light_sample but its shadow test -- whether the sample is lit, its unoccluded
+// contribution and the shadow ray (from the hit point along the unnormalised toLight)
+struct LightPrep { bool lit; V3 contrib, toLight; };
+D LightPrep lightPrep(const Ctx& c, const Hit& ins, V2 u2) {
+  LightPrep lp;
+  lp.lit = false; lp.contrib = v3s(0.0f); lp.toLight = v3s(0.0f);
   // randomInt(seed,0,ln) = int(random2(seed).x * ln): the same hash as the BSDF sample's first component
-  if (c.kLights == 0) return v3s(0.0f);                      // no light plugin compiled in
+  if (c.kLights == 0) return lp;                              // no light plugin compiled in
   const int index = to_int(u2.x * (float)c.ln);
-  if (c.ln <= 0) return v3s(0.0f);
+  if (c.ln <= 0) return lp;
   const int catRow = (index <= 0) ? 0 : c.ln - 1;           // readInt(lights, vec2(0, index)) : integer row coord
   const int cat = to_int(c.lt[catRow * 18]);
-  if (cat < 0 || cat >= 32 || !((c.lightMask >> cat) & 1u)) return v3s(0.0f);
+  if (cat < 0 || cat >= 32 || !((c.lightMask >> cat) & 1u)) return lp;
   const int row = (c.ln == 1) ? 0 : (index < 0 ? 0 : (index > c.ln - 1 ? c.ln - 1 : index));
   const float* L = c.lt + row * 18;
   V3 contrib = v3s(0.0f), toLight = v3s(0.0f);
@@ -1373,13 +1391,24 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
     contrib = em * fall * fmax_(0.0f, dot(normalize(toLight), ins.normal)) / (d * d);
     lit = true;
   }
-  if (!lit) return v3s(0.0f);
+  lp.lit = lit; lp.contrib = contrib; lp.toLight = toLight;
+  return lp;
+}
+D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
+  const LightPrep lp = lightPrep(c, ins, u2);
+  if (!lp.lit) return v3s(0.0f);
   // testShadow(Ray(hit, toLight)) (shader.light.js:24-31): unnormalised direction, no origin offset
-  if (testShadow(c, mkRay(ins.hit, toLight))) return v3s(0.0f);
-  return contrib;
+  if (testShadow(c, mkRay(ins.hit, lp.toLight))) return v3s(0.0f);
+  return lp.contrib;
 }
 
 // ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
+// SAIL_SHADOW_LATE=1: both outcomes of the shadow test, the throughput and the next ray before the shadow sweep
+// (shadeBounce), so that less state is live across it. Bit-identical, but the allocator answers with more spills
+// in the pre-cull kernel (172 scratch instructions instead of 94): C3 -0.9 %, C4 -12.8 %. Off.
+#ifndef SAIL_SHADOW_LATE
+#define SAIL_SHADOW_LATE 0
+#endif
 D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc);
 // fstrace.glsl:15-16 AOVs (normal/2 + 0.5, normalize(p)) of the first hit; a primary miss stores n = p = 0
 D void storeAov(float4* aovN, float4* aovP, size_t g, V3 n, V3 p) {
@@ -1448,6 +1477,35 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
     const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
 #endif
     PHASE_MARK(pc, 4);  // BSDF sample
+#if SAIL_SHADOW_LATE
+    if (c.kLights != 0) {
+      // Both outcomes of the shadow test are computed first -- direct = 0 + L * f with L the contribution (lit and
+      // unoccluded) or 0 -- then the throughput and the next ray, and the shadow sweep runs last with only its ray,
+      // the two radiance candidates, the throughput and the next ray live (not the hit record, BSDF value and
+      // contribution). Every value is the same expression as below.
+      const bool wantLight = isBlack(ins.emission) && ins.matCategory == SAIL_MATTE;
+      LightPrep lp;
+      lp.lit = false; lp.contrib = v3s(0.0f); lp.toLight = v3s(0.0f);
+      if (wantLight) lp = lightPrep(c, ins, u2);
+      const V3 dDark = wantLight ? v3s(0.0f) + v3s(0.0f) * f : v3s(0.0f);
+      const V3 eDark = e + (ins.emission + dDark) * fpdf;
+      V3 eLit = eDark;
+      if (lp.lit) eLit = e + (ins.emission + (v3s(0.0f) + lp.contrib * f)) * fpdf;
+      fpdf = fpdf * _fpdf;
+      const V3 shadowO = ins.hit, shadowD = lp.toLight;
+#if SAIL_AXIS_FRAME
+      const float outdot = ins.axis ? dotX(ins.normal, wi) : dot(ins.normal, wi);
+#else
+      const float outdot = dot(ins.normal, wi);
+#endif
+      ray = mkRay(ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f), wi);
+      bool dark = true;
+      if (lp.lit) dark = testShadow(c, mkRay(shadowO, shadowD));
+      e = dark ? eDark : eLit;
+      PHASE_MARK(pc, 5);  // light sample + shadow ray + next ray
+      return;
+    }
+#endif
     V3 direct = v3s(0.0f);
     if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) {
       if (c.kLights == 0)  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
