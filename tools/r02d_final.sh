@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-2 evidence (final kernels, last part of the round) in one GPU call: parity suite + smoke, rocprofv3 kernel stats of the C2 bench, PMC passes for
+# C2/C3/C4 (one counter group per run, kernel-trace only) summarised on the box into gpurun_out/summ/r02_*.json
+# and copied into profiles/ there, then the bench lines (C2 with the CPU baselines, C3, C4, C5 at a reduced spp)
+# so their traffic / VALU-issue fields read the fresh summaries. Every GPU step has its own limit; the script
+# stops at the first failure.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/final2
+mkdir -p $OUT gpurun_out/summ
+ROOT=$(pwd)
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 2; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 3; }
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof -o run --output-format csv -- \
+    python3 $ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $ROOT/$OUT/prof.log 2>&1 ) || { tail $OUT/prof.log; exit 4; }
+PMC_OUT=$OUT/pmc_c2 PMC_CONFIG=C2 PMC_SPP=64 bash tools/pmc.sh > /dev/null || exit 5
+PMC_OUT=$OUT/pmc_c3 PMC_CONFIG=C3 PMC_SPP=64 bash tools/pmc.sh > /dev/null || exit 6
+PMC_OUT=$OUT/pmc_c4 PMC_CONFIG=C4 PMC_SPP=32 bash tools/pmc.sh > /dev/null || exit 7
+python tools/pmc_summary.py $OUT/pmc_c2 gpurun_out/summ/r02_pmc_summary.json 2073600 32 8 cornell_box_readme_C2 > /dev/null || exit 8
+python tools/pmc_summary.py $OUT/pmc_c3 gpurun_out/summ/r02_pmc_summary_c3.json 2073600 32 8 materials_demo_C3 > /dev/null || exit 8
+python tools/pmc_summary.py $OUT/pmc_c4 gpurun_out/summ/r02_pmc_summary_c4.json 8294400 32 12 random64_C4 > /dev/null || exit 8
+cp gpurun_out/summ/r02_*.json profiles/
+timeout -k 10 400 python bench.py > $OUT/bench.log 2> $OUT/bench.err || { tail $OUT/bench.err; exit 9; }
+tail -1 $OUT/bench.log | cut -c1-300
+timeout -k 10 300 python bench.py --config C3 --steps 1 --warmup 1 --spp 128 --no-cpu-baseline > $OUT/bench_c3.log 2>&1 || exit 10
+timeout -k 10 300 python bench.py --config C4 --steps 1 --warmup 1 --spp 32 --no-cpu-baseline > $OUT/bench_c4.log 2>&1 || exit 11
+tail -1 $OUT/bench_c3.log | cut -c1-200; tail -1 $OUT/bench_c4.log | cut -c1-200
+
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof_c4 -o run --output-format csv -- \
+    python3 $ROOT/bench.py --config C4 --steps 1 --warmup 1 --spp 32 --no-cpu-baseline > $ROOT/$OUT/prof_c4.log 2>&1 ) || { tail $OUT/prof_c4.log; exit 12; }
+timeout -k 10 300 python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_c4_full.log 2>&1 || exit 13
+timeout -k 10 300 python bench.py --config C3 --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_c3_full.log 2>&1 || exit 14
+tail -1 $OUT/bench_c4_full.log | cut -c1-200; tail -1 $OUT/bench_c3_full.log | cut -c1-200
+echo final2 ok
