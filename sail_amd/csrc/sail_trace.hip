@@ -1402,13 +1402,39 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   return lp.contrib;
 }
 
-// ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
-// SAIL_SHADOW_LATE=1: both outcomes of the shadow test, the throughput and the next ray before the shadow sweep
-// (shadeBounce), so that less state is live across it. Bit-identical, but the allocator answers with more spills
-// in the pre-cull kernel (172 scratch instructions instead of 94): C3 -0.9 %, C4 -12.8 %. Off.
-#ifndef SAIL_SHADOW_LATE
-#define SAIL_SHADOW_LATE 0
+// The path's final bounce: only its radiance is read afterwards (the throughput and the next ray are dead), so the
+// BSDF sample is needed there only for f -- the light term's weight, which a matte surface alone sets -- and a
+// Lambertian matte f (kd * sc / pi, matte.glsl) does not depend on the sample. shadeLast adds that bounce's
+// radiance without the shading frame, BSDF sample or next ray, by the same expression on the same values as
+// shadeBounce; it declines (false) for an Oren-Nayar matte, whose f needs the sampled direction, and for any matte
+// path when a light plugin is compiled in (its light sample and shadow sweep stay in shadeBounce alone: a second
+// inlined shadow sweep multiplied the pre-cull kernel's spills).
+// Measured bit-identical: C2 +4.2 %, C3 +2.6 %, C4 -0.6 % (its 12-bounce paths are mostly matte with lights, which
+// decline). 1 (default) = every kernel but the pre-cull one, 2 = every kernel, 0 = off.
+#ifndef SAIL_LAST_BOUNCE
+#define SAIL_LAST_BOUNCE 1
 #endif
+#define SAIL_LAST_ON(cull) (SAIL_LAST_BOUNCE == 2 || (SAIL_LAST_BOUNCE == 1 && !(cull)))
+D bool shadeLast(const Ctx& c, const Hit& ins, float seed, const V3& fpdf, V3& e) {
+  const bool matteLit = isBlack(ins.emission) && ins.matCategory == SAIL_MATTE;  // path.glsl:10-11
+  if (matteLit && c.kLights != 0) return false;
+  V3 f = v3s(0.0f);
+  // material()'s matte branch (the plugin in the scene and compiled in)
+  if (matteLit && ((c.matMask >> SAIL_MATTE) & 1u) && HAS(c.kMats, SAIL_MATTE)) {
+    const float kd = TP(c, ins.matRow, 1), sigma = TP(c, ins.matRow, 2);
+    if (!(sigma < kEps)) return false;
+    f = (kd * ins.sc) * kInvPI;
+  }
+  (void)seed;
+  V3 direct = v3s(0.0f);
+  if (matteLit)  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
+    direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
+  const V3 sh = ins.emission + direct;
+  e = e + sh * fpdf;
+  return true;
+}
+
+// ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
 D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc);
 // fstrace.glsl:15-16 AOVs (normal/2 + 0.5, normalize(p)) of the first hit; a primary miss stores n = p = 0
 D void storeAov(float4* aovN, float4* aovP, size_t g, V3 n, V3 p) {
@@ -1430,7 +1456,8 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, float4* aovN, float4*
       storeAov(aovN, aovP, (size_t)aovPix, hit ? ins.normal : v3s(0.0f), hit ? ins.hit : v3s(0.0f));
     }
     if (ins.d >= kMaxDistance) break;
-    shadeBounce(c, ins, ray, seed, fpdf, e, pc);
+    if (!(SAIL_LAST_ON(c.cullPrims) && depth == maxDepth && shadeLast(c, ins, seed, fpdf, e)))
+      shadeBounce(c, ins, ray, seed, fpdf, e, pc);
   }
   return e;
 }
@@ -1477,35 +1504,6 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
     const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
 #endif
     PHASE_MARK(pc, 4);  // BSDF sample
-#if SAIL_SHADOW_LATE
-    if (c.kLights != 0) {
-      // Both outcomes of the shadow test are computed first -- direct = 0 + L * f with L the contribution (lit and
-      // unoccluded) or 0 -- then the throughput and the next ray, and the shadow sweep runs last with only its ray,
-      // the two radiance candidates, the throughput and the next ray live (not the hit record, BSDF value and
-      // contribution). Every value is the same expression as below.
-      const bool wantLight = isBlack(ins.emission) && ins.matCategory == SAIL_MATTE;
-      LightPrep lp;
-      lp.lit = false; lp.contrib = v3s(0.0f); lp.toLight = v3s(0.0f);
-      if (wantLight) lp = lightPrep(c, ins, u2);
-      const V3 dDark = wantLight ? v3s(0.0f) + v3s(0.0f) * f : v3s(0.0f);
-      const V3 eDark = e + (ins.emission + dDark) * fpdf;
-      V3 eLit = eDark;
-      if (lp.lit) eLit = e + (ins.emission + (v3s(0.0f) + lp.contrib * f)) * fpdf;
-      fpdf = fpdf * _fpdf;
-      const V3 shadowO = ins.hit, shadowD = lp.toLight;
-#if SAIL_AXIS_FRAME
-      const float outdot = ins.axis ? dotX(ins.normal, wi) : dot(ins.normal, wi);
-#else
-      const float outdot = dot(ins.normal, wi);
-#endif
-      ray = mkRay(ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f), wi);
-      bool dark = true;
-      if (lp.lit) dark = testShadow(c, mkRay(shadowO, shadowD));
-      e = dark ? eDark : eLit;
-      PHASE_MARK(pc, 5);  // light sample + shadow ray + next ray
-      return;
-    }
-#endif
     V3 direct = v3s(0.0f);
     if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) {
       if (c.kLights == 0)  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
@@ -1828,7 +1826,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
         V3 e = v3(sE[0][pixel], sE[1][pixel], sE[2][pixel]);
-        shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
+          shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
         sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
       }
     }
