@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 evidence (final kernels, last part of the round) in one GPU call: parity suite + smoke, rocprofv3 kernel stats of the C2 bench, PMC passes for
+# Round-2 evidence (final kernels, last part of the round; + C5 in full and the JS-host bench) in one GPU call: parity suite + smoke, rocprofv3 kernel stats of the C2 bench, PMC passes for
 # C2/C3/C4 (one counter group per run, kernel-trace only) summarised on the box into gpurun_out/summ/r02_*.json
 # and copied into profiles/ there, then the bench lines (C2 with the CPU baselines, C3, C4, C5 at a reduced spp)
 # so their traffic / VALU-issue fields read the fresh summaries. Every GPU step has its own limit; the script
@@ -31,4 +31,8 @@ tail -1 $OUT/bench_c3.log | cut -c1-200; tail -1 $OUT/bench_c4.log | cut -c1-200
 timeout -k 10 300 python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_c4_full.log 2>&1 || exit 13
 timeout -k 10 300 python bench.py --config C3 --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_c3_full.log 2>&1 || exit 14
 tail -1 $OUT/bench_c4_full.log | cut -c1-200; tail -1 $OUT/bench_c3_full.log | cut -c1-200
+timeout -k 10 300 python bench.py --config C5 --steps 1 --warmup 0 --no-cpu-baseline > $OUT/bench_c5_full.log 2>&1 || exit 15
+tail -1 $OUT/bench_c5_full.log | cut -c1-200
+timeout -k 10 300 node sail_amd/js/tools/bench_host.js > $OUT/bench_js_host.json 2> $OUT/bench_js_host.err || exit 16
+cut -c1-300 $OUT/bench_js_host.json
 echo final2 ok
