@@ -511,3 +511,38 @@ def test_coverage_kernel_selection(gpu, fixtures):
         ctx.set_scene_dict(fixtures["scenes"][name])
         assert ctx.kernel_name() == k, name
         ctx.close()
+
+
+# ---- the last-bounce shortcut (sail_trace.hip shadeLast) on the materials it must decline or pass NaN through ----
+# C1 uses the Cornell kernel (no light plugin), where shadeLast handles every path: Oren-Nayar matte (sigma > 0) must
+# decline to the full bounce (f needs the sampled direction); an infinite kd makes the matte f inf / NaN, which the
+# last bounce's direct term (0 + 0 * f) must carry into the radiance exactly as the full bounce does.
+LAST_BOUNCE_MATS = {
+    "oren_nayar": lambda tp: tp.__setitem__((slice(None), slice(2, 5)), np.where(tp[:, :1] == 1, [20.0, 0.6, 0.35], tp[:, 2:5])),
+    "inf_kd": lambda tp: tp.__setitem__((0, 1), np.inf),
+    "huge_kd": lambda tp: tp.__setitem__((2, 1), 3e38),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(LAST_BOUNCE_MATS))
+@pytest.mark.parametrize("B", [1, 3])
+def test_last_bounce_shortcut_edge_materials(gpu, fixtures, variant, B):
+    sc = dict(fixtures["scenes"]["C1"])
+    tp = np.array(sc["texparams"], dtype=np.float32).reshape(sc["tn"], 16)
+    LAST_BOUNCE_MATS[variant](tp)
+    sc["texparams"] = tp.reshape(-1).tolist()
+    W, H, spp = 24, 20, 3
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    ctx = capi.Context(W, H)
+    try:
+        ctx.set_scene_dict(sc)
+        assert ctx.kernel_name() == "sail_trace_kernel_cornell"
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got = ctx.read_accum()
+    finally:
+        ctx.close()
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    same = bit_equal(got, want)
+    assert same.all(), f"{variant}, {B} bounces: {int((~same).sum())} channels differ"
+    if variant == "inf_kd":
+        assert np.isnan(got[..., :3]).any() or np.isinf(got[..., :3]).any()
