@@ -1679,7 +1679,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 // wider barrier.
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
-  static_assert(NT == 256 || ((NT == 512 || NT == 1024) && !GROUPED), "grouped kernels share the 256-thread stage layout");
+  static_assert(NT == 256 || ((NT == 128 || NT == 512 || NT == 1024) && !GROUPED), "grouped kernels share the 256-thread stage layout");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
   __shared__ float sSt[kFields][NT];
@@ -2181,7 +2181,7 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
 #define SAIL_LAUNCH_NT(k, nt)                                                                   \
   do {                                                                                          \
     if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks), dim3(256), 0, s, A);                   \
-    else hipLaunchKernelGGL(k, dim3(blocks / ((nt) / 256)), dim3(nt), 0, s, A);                 \
+    else hipLaunchKernelGGL(k, dim3(blocks * 256 / (nt)), dim3(nt), 0, s, A);                     \
   } while (0)
   if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT);
   else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT);
