@@ -1674,6 +1674,14 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
+// SAIL_END_DEFER: no end-of-sample barriers. Sample k's radiance is read back by its pixel's lane after the first
+// sort barrier of sample k + 1 (every write of sample k precedes it; sample k + 1 writes the slot only after the
+// scatter barrier), the first bounce starts from 0 instead of a cleared slot, and a path that misses at once clears
+// its own slot there. The last sample is read after one barrier at the end. Bit-identical, measured slower (the
+// read-back and accumulation inlined into the bounce loop: C2 -2.3 %, C3 -6.6 %, C4 -2.2 %), so off.
+#ifndef SAIL_END_DEFER
+#define SAIL_END_DEFER 0
+#endif
 // SAIL_SORT_2BAR: two barriers per bounce instead of three (every wave scans double-buffered counts itself):
 // 1 = every kernel, 2 = the pre-cull kernel only. Bit-identical; C2 -3.4 %, C3 -0.5 %, C4 +0.9 % (measured)
 #ifndef SAIL_SORT_2BAR
@@ -1743,6 +1751,18 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   for (int q = 0; q < 8; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
+  // SAIL_END_DEFER (needs a first bounce, whose sort barrier orders the read-back)
+  const bool deferRead = SAIL_END_DEFER && A.maxBounces >= 1;
+  int kPrev = -1;
+  // sample kPrev's radiance into the accumulator / stage; a path that missed at once (dead) clears its slot
+  auto settlePrev = [&](bool alive) {
+    if (valid && kPrev >= 0) {
+      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
+      if (grouped) stageSample(A, kPrev, tw.bid, li, er);
+      else accumulateSample(acc, er, constRow<SailSample>(A.samples, kPrev), A.accumMode);
+    }
+    if (!alive) { sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f; }
+  };
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = constRow<SailSample>(A.samples, k);
     const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
@@ -1756,7 +1776,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     }
     V3 fpdf = v3s(1.0f);
     // the path's radiance lives in LDS at its pixel: one path per pixel, updated in bounce order
-    sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f;
+    if (!deferRead) { sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f; }
     for (int depth = 1; depth <= A.maxBounces; depth++) {
       Sweep sw;
       sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
@@ -1795,6 +1815,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       // cleared by wave 0 after the scatter barrier, two bounces before it is counted into again
       if (alive) rank = atomicAdd(&sCnt2[ph][key], 1);
       __syncthreads();
+      if (deferRead && depth == 1) settlePrev(alive);
       {
         const int v = sCnt2[ph][lane];
         int incl = v;
@@ -1820,6 +1841,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int* const sCnt = sCnt2[0];
       if (alive) rank = atomicAdd(&sCnt[key], 1);
       __syncthreads();
+      if (deferRead && depth == 1) settlePrev(alive);
       if (wave == 0) {
         const int v = sCnt[lane];
         int incl = v;
@@ -1863,12 +1885,13 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
-        V3 e = v3(sE[0][pixel], sE[1][pixel], sE[2][pixel]);
+        V3 e = (deferRead && depth == 1) ? v3s(0.0f) : v3(sE[0][pixel], sE[1][pixel], sE[2][pixel]);
         if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
           shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
         sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
       }
     }
+    if (deferRead) { kPrev = k; continue; }
     __syncthreads();
     if (valid) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
@@ -1876,6 +1899,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
+  }
+  if (deferRead && kPrev >= 0) {
+    __syncthreads();
+    settlePrev(true);
   }
   if (valid && !grouped) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
