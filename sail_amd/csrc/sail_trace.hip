@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include "sail_device.h"
 #include "sail_math.h"
+#include "sail_scan.h"
 
 using namespace sm;
 
@@ -1674,6 +1675,10 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
+// the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
+#ifndef SAIL_SCAN_DPP
+#define SAIL_SCAN_DPP 1
+#endif
 // SAIL_END_DEFER: no end-of-sample barriers. Sample k's radiance is read back by its pixel's lane after the first
 // sort barrier of sample k + 1 (every write of sample k precedes it; sample k + 1 writes the slot only after the
 // scatter barrier), the first bounce starts from 0 instead of a cleared slot, and a path that misses at once clears
@@ -1818,11 +1823,15 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       if (deferRead && depth == 1) settlePrev(alive);
       {
         const int v = sCnt2[ph][lane];
+#if SAIL_SCAN_DPP
+        const int incl = waveScanIncl(v);
+#else
         int incl = v;
         for (int off = 1; off < 64; off <<= 1) {
           const int u = __shfl_up(incl, off, 64);
           if (lane >= off) incl += u;
         }
+#endif
         nAlive = __shfl(incl, 63, 64);
         const int start = __shfl(incl - v, key, 64);
         if (alive) {
@@ -1844,11 +1853,15 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       if (deferRead && depth == 1) settlePrev(alive);
       if (wave == 0) {
         const int v = sCnt[lane];
+#if SAIL_SCAN_DPP
+        const int incl = waveScanIncl(v);
+#else
         int incl = v;
         for (int off = 1; off < 64; off <<= 1) {
           const int u = __shfl_up(incl, off, 64);
           if (lane >= off) incl += u;
         }
+#endif
         sStart[lane] = incl - v;
         if (lane == 63) sStart[kKeys] = incl;
         sCnt[lane] = 0;

@@ -5,7 +5,7 @@
 # so their traffic / VALU-issue fields read the fresh summaries. Every GPU step has its own limit; the script
 # stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/final2
+OUT=gpurun_out/${FINAL_OUT:-final2}
 mkdir -p $OUT gpurun_out/summ
 ROOT=$(pwd)
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 2; }
