@@ -1688,9 +1688,11 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #define SAIL_END_DEFER 0
 #endif
 // SAIL_SORT_2BAR: two barriers per bounce instead of three (every wave scans double-buffered counts itself):
-// 1 = every kernel, 2 = the pre-cull kernel only. Bit-identical; C2 -3.4 %, C3 -0.5 %, C4 +0.9 % (measured)
+// 1 = every kernel, 2 = the pre-cull kernel only, 3 = the pre-cull and room kernels. Bit-identical; measured with the
+// shuffle scan C2 -3.4 %, C3 -0.5 %, C4 +0.9 %; with the DPP scan and the live count by readlane C2 -1.0 %, C3 +1.1 %
+// (twice), C4 +1.3-1.7 % over the bpermute count
 #ifndef SAIL_SORT_2BAR
-#define SAIL_SORT_2BAR 2
+#define SAIL_SORT_2BAR 3
 #endif
 // NT threads per workgroup (ungrouped kernels only; grouped ones keep 256): a 16 x NT/16 pixel block, 4096/NT
 // blocks per 64x64 tile. A larger workgroup sorts a larger pool of paths (fewer mixed waves) at the price of a
@@ -1702,7 +1704,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr int kFields = 15;
   __shared__ float sSt[kFields][NT];
   __shared__ float sE[3][NT];
-  constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR == 2 && CULL);
+  constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
+                          (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
   TileWork tw = tileWork<GROUPED>(A);
@@ -1832,7 +1835,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (lane >= off) incl += u;
         }
 #endif
-        nAlive = __shfl(incl, 63, 64);
+        nAlive = __builtin_amdgcn_readlane(incl, 63);
         const int start = __shfl(incl - v, key, 64);
         if (alive) {
           const int d = start + rank;
