@@ -172,6 +172,45 @@ def valu_issue(pmc, avg_launch_s, device):
             "frac": round(achieved / peak, 4), "lane_utilisation": round(pmc.get("derived", {}).get("valu_lane_utilisation", 0.0), 3)}
 
 
+def validate_frame(ctx, sc, masks, mvp, W, H, B, spp, inv, seeds, part, ngpu):
+    """After the timed steps: the reduced frame on rank 0 must be the whole frame. Every pixel counts each sample
+    exactly once (a reduce that drops or double-counts a rank's tiles or samples fails this), and small crops in
+    tiles of different ranks equal the CPU oracle's render of the same samples (the checker, run outside the timed
+    region): bit for bit for a tile split, to summation order for a sample split. Returns a report; raises
+    SystemExit if the frame is wrong, so no number is printed for it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle  # test infrastructure: the CPU checker of the frame the GPUs produced
+    acc = ctx.read_accum()
+    counts = acc[..., 3]
+    bad_counts = int(np.count_nonzero(counts != np.float32(spp)))
+    tx, ty = (W + 63) // 64, (H + 63) // 64
+    ntiles = tx * ty
+    # one crop in a tile of rank 0, of rank N-1 and in the last tile (a ragged one when W or H is not a multiple of 64)
+    tiles = sorted({0, min(ngpu - 1, ntiles - 1), ntiles - 1})
+    c = 4 if W * H * spp * B <= 2e10 else 2  # C4 / C5: smaller crops keep the oracle under a few seconds
+    crops, worst = [], 0.0
+    for t in tiles:
+        x0 = (t % tx) * 64 + min(30, (W - (t % tx) * 64) // 2)
+        y0 = (t // tx) * 64 + min(30, (H - (t // tx) * 64) // 2)
+        x0, y0 = min(x0, W - c), min(y0, H - c)
+        want = oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c))[y0:y0 + c, x0:x0 + c]
+        got = acc[y0:y0 + c, x0:x0 + c]
+        if part == capi.PART_TILES or ngpu == 1:
+            ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        else:
+            ok = bool(np.allclose(got, want, rtol=1e-4, atol=1e-6))
+        worst = max(worst, float(np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-6))))
+        crops.append({"tile": t, "rank": t % ngpu if part == capi.PART_TILES else "all", "x0": x0, "y0": y0,
+                      "size": c, "match": ok})
+    rep = {"pixels_with_wrong_count": bad_counts, "expected_count": spp, "oracle_crops": crops,
+           "rule": "bit-exact" if (part == capi.PART_TILES or ngpu == 1) else "summation order (rtol 1e-4)",
+           "max_rel_diff": worst}
+    if bad_counts or not all(cr["match"] for cr in crops):
+        print(json.dumps({"error": "reduced frame failed validation", "validation": rep}), file=sys.stderr, flush=True)
+        raise SystemExit(3)
+    return rep
+
+
 class _StdoutToStderr:
     """Points file descriptor 1 at stderr (C-level prints included) between __enter__ and __exit__."""
 
@@ -203,6 +242,10 @@ def main():
     ap.add_argument("--launch-spp", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c1-full", action="store_true", help="skip the ~30 s full C1 render of the CPU baseline")
+    ap.add_argument("--force-rccl", action="store_true",
+                    help="one process: the multi-device context's RCCL reduce even at --gpus 1 (SAIL_DEBUG_FORCE_RCCL)")
+    ap.add_argument("--no-validate", action="store_true",
+                    help="skip the check of the reduced frame after the timed steps (counts + oracle crops)")
     ap.add_argument("--force-comm", action="store_true",
                     help="exercise the torch.distributed + RCCL reduce path even with one rank")
     args = ap.parse_args()
@@ -212,8 +255,9 @@ def main():
     if args.gpus < 1 or (world > 1 and args.gpus != world):
         sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE {world} (one process per GPU under "
                  "torch.distributed.run, or --gpus N in one process)")
-    # one process, N GPUs: the library's multi-device context splits the frame (no torch.distributed)
-    multi = world == 1 and args.gpus > 1
+    # one process, N GPUs: the library's multi-device context splits the frame (no torch.distributed);
+    # --force-rccl takes that path (ncclCommInitAll + the grouped reduce) at one GPU too
+    multi = world == 1 and (args.gpus > 1 or args.force_rccl)
     if multi and capi.device_count() < args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but only {capi.device_count()} HIP devices are visible")
     # RCCL prints its version banner on stdout when a communicator is created; the contract is ONE JSON line
@@ -240,6 +284,8 @@ def main():
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
 
     ctx = capi.Context(W, H, devices=list(range(args.gpus))) if multi else capi.Context(W, H, device=local_rank)
+    if multi and args.force_rccl:
+        ctx.set_debug(capi.DEBUG_FORCE_RCCL, 1)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
     part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
@@ -292,6 +338,9 @@ def main():
     total_segments = W * H * spp * B * args.steps  # nominal; closed scene: every path runs all bounces
     value = total_segments / elapsed / 1e6
     ngpu = args.gpus if multi else world
+    validation = None
+    if rank == 0 and not args.no_validate:  # after the timed region: the frame the steps produced is checked
+        validation = validate_frame(ctx, sc, masks, mvp, W, H, B, spp, inv, seeds, part, ngpu)
     if rank == 0:
         avg_launch_s = (kernel_ms / max(launches, 1)) / 1e3
         # this rank's pixels per launch (rank 0 at N = 1: the full frame)
@@ -337,6 +386,7 @@ def main():
                 "valu_issue": valu_issue(pmc, avg_launch_s, local_rank),
             },
         }
+        rec["validation"] = validation
         if flt:
             fms = ctx.filter_ms()
             fbytes = W * H * (16 + 16)  # mean-image read once from HBM (taps hit L2) + float4 write

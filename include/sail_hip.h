@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SAIL_ABI_VERSION 2
+#define SAIL_ABI_VERSION 3
 
 enum sail_status {
   SAIL_OK = 0,
@@ -105,12 +105,21 @@ enum sail_debug_option {
   SAIL_DEBUG_CULL_MIN_PRIMS = 1, /* scenes with >= value primitives use the padded-box pre-cull kernel [8] */
   SAIL_DEBUG_FORCE_GENERIC = 2,  /* 1: always launch the all-plugin kernel [0] */
   SAIL_DEBUG_CULL_FMA = 3,       /* 0: the plain pre-cull slab form instead of the fused one [1] */
-  SAIL_DEBUG_SAMPLE_GROUPS = 4   /* > 0: fixed sample-group count per 16x16 block [0 = sized by occupancy] */
+  SAIL_DEBUG_SAMPLE_GROUPS = 4,  /* > 0: fixed sample-group count per 16x16 block [0 = sized by occupancy] */
+  /* multi-device contexts of distinct devices only: 1 builds the ncclCommInitAll communicator now even for ONE
+   * device, so the grouped RCCL reduce (the path of N distinct GPUs) runs on a one-GPU machine [0: a one-device
+   * context needs no reduce]. Refused (SAIL_E_INVALID) on a context whose devices are all the same GPU. */
+  SAIL_DEBUG_FORCE_RCCL = 5
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 
 /* Tracer.render(mvp, eye, k) (src/core/tracer.js:92-101) = one progressive sample with the caller's
- * jittered inverse matrix (16 f32, column-major as uniformMatrix4fv uploads it, webgl.js:103) and seed. */
+ * jittered inverse matrix (16 f32, column-major as uniformMatrix4fv uploads it, webgl.js:103) and seed.
+ * One-sample frames are queued and launched together (up to sail_set_launch_samples of them per launch) when
+ * nothing observes the frame in between: every entry point that reads, filters, reduces, counts or changes the
+ * context launches the queue first, and a change of eye or bounce count launches it before the new sample is
+ * queued. The frame is bit-identical to one launch per call (samples are accumulated in the same order); a
+ * launch error of a queued sample is reported by the call that launches it. */
 int sail_render(sail_ctx* ctx, const float inv_mvp[16], const float eye[3], float time_seed, int max_bounces);
 /* spp samples in one call: inv_mvp = spp x 16 floats, seeds = spp floats (a deterministic schedule). */
 int sail_render_schedule(sail_ctx* ctx, const float* inv_mvp, const float* seeds, const float eye[3],
@@ -134,6 +143,21 @@ int sail_pick(sail_ctx* ctx, const float* rays, int count, int32_t* index, float
 int sail_filter(sail_ctx* ctx, int kind, const float* weights16, float rx, float ry, float gamma_c,
                 float* out_rgba, uint8_t* out_rgba8);
 int sail_get_stats(sail_ctx* ctx, sail_stats* out);
+
+/* ---- checkpoint / resume of a progressive render (no reference counterpart: the reference restarts its
+ * accumulation on every camera or object change, src/core/renderer.js:57-60, src/scene/scene.js:65-68) ----
+ * A context's accumulation is `parts` raw accumulators (1 for sail_create, one per device for sail_create_multi),
+ * each W*H*4 f32 in sail_read_accum's layout, plus the global sample index k of the next sample. Saving every part
+ * and loading them into a fresh context with the same size, scene, partition and accumulation mode continues the
+ * render bit for bit: render k -> save -> new context -> load -> render k more == the 2k-sample frame. */
+int sail_accum_parts(sail_ctx* ctx, int* parts);
+/* copy accumulator `part` (this rank's own, never the reduced frame) and the sample index k */
+int sail_save_accum(sail_ctx* ctx, int part, float* sums, uint64_t* k);
+/* replace accumulator `part` by `sums` and set the sample index to k (every part of the context). part = -1 loads a
+ * whole-frame accumulator (sail_read_accum of a reduced frame): on a multi-device context each device keeps its own
+ * tiles of it (tile partition) or device 0 takes all of it (sample partition: equal to the uninterrupted render to
+ * summation order only; load the parts for bit-exactness). The AOVs restart with the next sample. */
+int sail_load_accum(sail_ctx* ctx, int part, const float* sums, uint64_t k);
 
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */
 /* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):
@@ -160,10 +184,13 @@ int sail_comm_init(sail_ctx* ctx, const char id[128], int nranks, int rank);
  * separate frame on `root`; collective: every rank calls it, all created with the same flags. The ranks'
  * accumulators are left as they are, so render -> reduce -> render -> reduce is progressive: each reduce sums
  * the cumulative accumulators afresh. On root, readback / read_accum / filter show that frame until the next
- * sail_render* or sail_reset (then this rank's own accumulator again). Asynchronous RCCL errors are reported
+ * sail_render* or sail_reset (then this rank's own accumulator again). With a sample partition the AOVs shown are
+ * those of the rank that rendered the frame's last sample, as on one GPU. Asynchronous RCCL errors are reported
  * here and by sail_sync (ncclCommGetAsyncError). On a multi-device context it reduces into device 0 (root 0). */
 int sail_reduce(sail_ctx* ctx, int root);
-int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes); /* this rank's (device 0's) accumulator */
+/* this rank's own accumulator (device 0's on a multi-device context), never the reduced frame: since ABI v2 the
+ * reduce is out of place, so after sail_reduce the pointer still holds rank-local sums */
+int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes);
 /* the 64x64 tiles rank `rank` of `world` owns in a W x H frame (tile t -> rank t % world), as
  * (x0, y0, w, h) quadruples; returns the tile count (or a negative error); out may be NULL to count */
 int sail_partition_tiles(int width, int height, int rank, int world, int* out_xywh, int capacity);

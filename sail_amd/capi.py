@@ -23,7 +23,7 @@ PART_TILES, PART_SAMPLES = 0, 1
 FILTER_COLOR, FILTER_GAMMA, FILTER_TONEMAPPING, FILTER_WINDOW = 0, 1, 2, 3
 FILTER_WAVELET, FILTER_NORMAL, FILTER_POSITION = 4, 5, 6  # need FLAG_AOV
 # sail_set_debug options (test / study switches; none changes a result)
-DEBUG_CULL_MIN_PRIMS, DEBUG_FORCE_GENERIC, DEBUG_CULL_FMA, DEBUG_SAMPLE_GROUPS = 1, 2, 3, 4
+DEBUG_CULL_MIN_PRIMS, DEBUG_FORCE_GENERIC, DEBUG_CULL_FMA, DEBUG_SAMPLE_GROUPS, DEBUG_FORCE_RCCL = 1, 2, 3, 4, 5
 # applied to every Context at creation (tests set entries with monkeypatch.setitem)
 DEBUG_DEFAULTS: dict = {}
 
@@ -35,7 +35,7 @@ EXPORTS = (
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
     "sail_prim_bounds", "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
-    "sail_abi_version",
+    "sail_abi_version", "sail_accum_parts", "sail_save_accum", "sail_load_accum",
 )
 
 
@@ -124,6 +124,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_pick": (ctypes.c_int, [vp, f32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), f32p]),
         "sail_kernel_name": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int]),
         "sail_filter_ms": (ctypes.c_int, [vp, f64p]),
+        "sail_accum_parts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+        "sail_save_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.POINTER(ctypes.c_uint64)]),
+        "sail_load_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -365,6 +368,27 @@ class Context:
 
     def reduce(self, root: int = 0):
         self._check(self.lib.sail_reduce(self.h, root), "sail_reduce")
+
+    def save(self) -> dict:
+        """Checkpoint of the progressive render: {"k": next sample index, "parts": [W x H x 4 f32 accumulator per
+        device]} (sail_save_accum)"""
+        n = ctypes.c_int(0)
+        self._check(self.lib.sail_accum_parts(self.h, ctypes.byref(n)), "sail_accum_parts")
+        parts, k = [], ctypes.c_uint64(0)
+        for i in range(n.value):
+            a = np.zeros((self.H, self.W, 4), dtype=np.float32)
+            self._check(self.lib.sail_save_accum(self.h, i, _ptr(a), ctypes.byref(k)), "sail_save_accum")
+            parts.append(a)
+        return {"k": int(k.value), "parts": parts}
+
+    def load(self, ckpt: dict):
+        """Resume from save()'s checkpoint (every part), or from a whole-frame accumulator
+        {"k": k, "frame": W x H x 4} (sail_load_accum part -1)"""
+        if "frame" in ckpt:
+            self._check(self.lib.sail_load_accum(self.h, -1, _ptr(_f32(ckpt["frame"])), int(ckpt["k"])), "sail_load_accum")
+            return
+        for i, a in enumerate(ckpt["parts"]):
+            self._check(self.lib.sail_load_accum(self.h, i, _ptr(_f32(a)), int(ckpt["k"])), "sail_load_accum")
 
     def accum_device_ptr(self):
         p = ctypes.c_void_p()

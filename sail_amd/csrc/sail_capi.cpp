@@ -165,6 +165,10 @@ struct sail_ctx {
   std::vector<nccl_comm_t> groupComms;
   bool groupLocal = false;
   bool dirty = false;
+  // One-sample frames of sail_render waiting to be launched together (sail_render / flushQueued): their records
+  // (global sample index already counted in k), the bounce count and eye they were queued with
+  std::vector<SailSample> queued;
+  int queuedBounces = 0;
   float eyeCache[3] = {0.0f, 0.0f, 0.0f};
   std::string err;
 };
@@ -257,6 +261,7 @@ void cornerDirs(const float* M, const float* eye, float out[4][3]) {
 
 int resetAccum(sail_ctx* c) {
   c->reduced = false;
+  c->queued.clear();  // queued one-sample frames belong to the accumulation being discarded
   const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
   HIPCHK(c, hipMemsetAsync(c->accum, 0, bytes, c->stream));
   if (c->aovN) HIPCHK(c, hipMemsetAsync(c->aovN, 0, bytes, c->stream));
@@ -635,6 +640,16 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   return SAIL_OK;
 }
 
+// Launch the queued one-sample frames of sail_render as one launch sequence (launchTrace splits it into launches of
+// launchSpp samples). Their sample index and counts were taken when they were queued.
+int flushQueued(sail_ctx* c) {
+  if (c->queued.empty()) return SAIL_OK;
+  std::vector<SailSample> q;
+  q.swap(c->queued);
+  HIPCHK(c, hipSetDevice(c->device));
+  return launchTrace(c, q.data(), (int)q.size(), c->queuedBounces);
+}
+
 // ---- reduced frame (sail_reduce, multi-device contexts) -----------------------------------------------------------
 int ensureFrame(sail_ctx* c) {
   const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
@@ -667,18 +682,29 @@ int groupCommCheck(sail_ctx* g) {
   return SAIL_OK;
 }
 
+// The sample-partition rank (device) that rendered the frame's last sample: its AOVs are the frame's, as on one GPU
+// (sample k is rendered by rank k % world; k = the context's sample count)
+int aovOwner(uint64_t k, int world) { return k > 0 ? (int)((k - 1) % (uint64_t)world) : 0; }
+// -0 in every component: the additive identity that keeps each AOV bit (x + -0 == x for +-0 and NaN too)
+hipError_t fillNegZero(float4* p, size_t np, hipStream_t s) {
+  return hipMemsetD32Async((hipDeviceptr_t)p, (int)0x80000000u, np * 4, s);
+}
+
 // Multi-device context: device 0's frame = the sum of every device's cumulative accumulator (and, for tile
 // partitions, of the AOV maps: -0 outside each device's tiles, so the sum is exact). Recomputed from scratch
 // whenever something was rendered since the last one, so progressive frames never count a sample twice.
-// Sample partitions show device 0's AOVs (each device's maps hold its own last sample).
+// Sample partitions show the AOVs of the device that rendered the last sample: in the RCCL reduce every other
+// device contributes a -0 map, so the reduced maps are that device's bits (the tile reduce's rule).
 int groupReduce(sail_ctx* g) {
   const int nd = (int)g->subs.size();
   sail_ctx* r = g->subs[0];
-  if (nd == 1 || !g->dirty) return SAIL_OK;
+  for (sail_ctx* s : g->subs) if (int rc = flushQueued(s)) return relay(g, rc, s);
+  if ((nd == 1 && g->groupComms.empty()) || !g->dirty) return SAIL_OK;
   HIPCHK(g, hipSetDevice(r->device));
   if (int rc = ensureFrame(r)) return relay(g, rc, r);
   const bool tiles = g->partMode == SAIL_PART_TILES;
   const size_t np = (size_t)g->W * g->H, bytes = np * sizeof(float4);
+  const int owner = aovOwner(r->k, nd);
   if (g->groupLocal) {  // every "device" is the same GPU: wait for the others' streams, sum in rank order
     for (sail_ctx* s : g->subs) HIPCHK(g, hipStreamSynchronize(s->stream));
     auto sum = [&](float4* dst, float4* sail_ctx::*src) -> hipError_t {
@@ -688,31 +714,64 @@ int groupReduce(sail_ctx* g) {
       for (int i = 0; i < nd; i++) A.src[i] = g->subs[i]->*src;
       return sail_launch_sum(A, r->stream);
     };
+    const sail_ctx* o = g->subs[owner];
     HIPCHK(g, sum(r->frame, &sail_ctx::accum));
-    if (r->aovN) HIPCHK(g, tiles ? sum(r->frameN, &sail_ctx::aovN) : hipMemcpyAsync(r->frameN, r->aovN, bytes, hipMemcpyDeviceToDevice, r->stream));
-    if (r->aovP) HIPCHK(g, tiles ? sum(r->frameP, &sail_ctx::aovP) : hipMemcpyAsync(r->frameP, r->aovP, bytes, hipMemcpyDeviceToDevice, r->stream));
+    if (r->aovN) HIPCHK(g, tiles ? sum(r->frameN, &sail_ctx::aovN) : hipMemcpyAsync(r->frameN, o->aovN, bytes, hipMemcpyDeviceToDevice, r->stream));
+    if (r->aovP) HIPCHK(g, tiles ? sum(r->frameP, &sail_ctx::aovP) : hipMemcpyAsync(r->frameP, o->aovP, bytes, hipMemcpyDeviceToDevice, r->stream));
     HIPCHK(g, hipStreamSynchronize(r->stream));  // the other devices' next renders may overwrite their inputs
   } else {  // one grouped RCCL reduce into device 0 over the ncclCommInitAll communicator
+    const bool aov = r->aovN || r->aovP;
+    if (!tiles && aov) {  // every device but the owner sends a -0 map (its frameN / frameP, device 0's in place)
+      for (int i = 0; i < nd; i++) {
+        sail_ctx* s = g->subs[i];
+        HIPCHK(g, hipSetDevice(s->device));
+        if (int rc = ensureFrame(s)) return relay(g, rc, s);
+        if (i != owner) {
+          if (s->frameN) HIPCHK(g, fillNegZero(s->frameN, np, s->stream));
+          if (s->frameP) HIPCHK(g, fillNegZero(s->frameP, np, s->stream));
+        }
+      }
+    }
     int e = g_rccl.groupStart();
     for (int i = 0; i < nd && e == 0; i++) {
       sail_ctx* s = g->subs[i];
       if (hipSetDevice(s->device) != hipSuccess) { e = -1; break; }
       e = g_rccl.reduce(s->accum, i == 0 ? r->frame : s->accum, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
-      if (e == 0 && tiles && s->aovN)
-        e = g_rccl.reduce(s->aovN, i == 0 ? r->frameN : s->aovN, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
-      if (e == 0 && tiles && s->aovP)
-        e = g_rccl.reduce(s->aovP, i == 0 ? r->frameP : s->aovP, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
+      const bool own = tiles || i == owner;  // the send buffer of this device's AOV maps
+      if (e == 0 && s->aovN)
+        e = g_rccl.reduce(own ? s->aovN : s->frameN, i == 0 ? r->frameN : (own ? s->aovN : s->frameN), np * 4,
+                          kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
+      if (e == 0 && s->aovP)
+        e = g_rccl.reduce(own ? s->aovP : s->frameP, i == 0 ? r->frameP : (own ? s->aovP : s->frameP), np * 4,
+                          kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
     }
     const int e2 = g_rccl.groupEnd();
     if (e || e2) return fail(g, SAIL_E_RCCL, "grouped ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(e ? e : e2) : "?");
     HIPCHK(g, hipSetDevice(r->device));
-    if (!tiles && r->aovN) HIPCHK(g, hipMemcpyAsync(r->frameN, r->aovN, bytes, hipMemcpyDeviceToDevice, r->stream));
-    if (!tiles && r->aovP) HIPCHK(g, hipMemcpyAsync(r->frameP, r->aovP, bytes, hipMemcpyDeviceToDevice, r->stream));
     if (int rc = groupCommCheck(g)) return rc;
   }
   r->reduced = true;
   g->dirty = false;
   return SAIL_OK;
+}
+
+// Host copy of a whole-frame accumulator keeping only what partition (rank, world, mode) holds: its own tiles, or
+// (sample partition) everything on rank 0 and nothing elsewhere (sail_load_accum part -1)
+void ownedPart(const sail_ctx* c, const float* sums, std::vector<float>& out) {
+  const size_t np = (size_t)c->W * c->H;
+  out.assign(np * 4, 0.0f);
+  if (c->world <= 1) { memcpy(out.data(), sums, np * 4 * sizeof(float)); return; }
+  if (c->partMode == SAIL_PART_SAMPLES) {
+    if (c->rank == 0) memcpy(out.data(), sums, np * 4 * sizeof(float));
+    return;
+  }
+  const int tx = (c->W + 63) / 64;
+  for (int y = 0; y < c->H; y++)
+    for (int x = 0; x < c->W; x++)
+      if (((y >> 6) * tx + (x >> 6)) % c->world == c->rank) {
+        const size_t i = ((size_t)y * c->W + x) * 4;
+        memcpy(&out[i], &sums[i], 4 * sizeof(float));
+      }
 }
 
 }  // namespace
@@ -823,6 +882,8 @@ int sail_create_multi(sail_ctx** out, int width, int height, const int* devices,
   *out = nullptr;
   std::vector<int> dev((size_t)n_devices);
   for (int i = 0; i < n_devices; i++) dev[i] = devices ? devices[i] : i;
+  for (int i = 0; i < n_devices; i++)  // a negative ordinal is the current device (sail_create's rule), resolved first
+    if (dev[i] < 0 && hipGetDevice(&dev[i]) != hipSuccess) return fail(nullptr, SAIL_E_HIP, "sail_create_multi: hipGetDevice");
   bool allSame = true, allDistinct = true;
   for (int i = 0; i < n_devices; i++)
     for (int j = 0; j < n_devices; j++) {
@@ -862,7 +923,31 @@ int sail_create_multi(sail_ctx** out, int width, int height, const int* devices,
 
 int sail_set_debug(sail_ctx* c, int option, int value) {
   if (!c) return SAIL_E_INVALID;
+  if (option == SAIL_DEBUG_FORCE_RCCL) {  // the multi-device context's own communicator, not its devices'
+    if (c->subs.empty() || c->groupLocal)
+      return fail(c, SAIL_E_INVALID, "SAIL_DEBUG_FORCE_RCCL needs a multi-device context of distinct devices");
+    for (sail_ctx* s : c->subs) if (int rc = flushQueued(s)) return relay(c, rc, s);
+    const int nd = (int)c->subs.size();
+    if (value && c->groupComms.empty()) {
+      if (!g_rccl.load()) return fail(c, SAIL_E_RCCL, "librccl not loadable");
+      std::vector<int> dev((size_t)nd);
+      for (int i = 0; i < nd; i++) dev[i] = c->subs[i]->device;
+      c->groupComms.assign((size_t)nd, nullptr);
+      const int r = g_rccl.commInitAll(c->groupComms.data(), nd, dev.data());
+      if (r) {
+        c->groupComms.clear();
+        return fail(c, SAIL_E_RCCL, "ncclCommInitAll: %s", g_rccl.errStr ? g_rccl.errStr(r) : "?");
+      }
+    } else if (!value && nd == 1 && !c->groupComms.empty()) {
+      for (sail_ctx* s : c->subs) { (void)hipSetDevice(s->device); (void)hipStreamSynchronize(s->stream); }
+      for (nccl_comm_t cm : c->groupComms) if (cm) g_rccl.commDestroy(cm);
+      c->groupComms.clear();
+    }
+    c->dirty = true;
+    return SAIL_OK;
+  }
   for (sail_ctx* s : c->subs) if (int rc = sail_set_debug(s, option, value)) return relay(c, rc, s);
+  if (int rc = flushQueued(c)) return rc;  // queued samples launch with the settings they were queued under
   switch (option) {
     case SAIL_DEBUG_CULL_MIN_PRIMS: c->cullMinPrims = value; break;
     case SAIL_DEBUG_FORCE_GENERIC: c->forceGeneric = value; break;
@@ -999,6 +1084,7 @@ int sail_set_launch_samples(sail_ctx* c, int spp) {
   if (!c) return SAIL_E_INVALID;
   if (spp < 1 || spp > 1 << 20) return fail(c, SAIL_E_INVALID, "launch samples %d", spp);
   for (sail_ctx* s : c->subs) if (int rc = sail_set_launch_samples(s, spp)) return relay(c, rc, s);
+  if (int rc = flushQueued(c)) return rc;
   c->launchSpp = spp;
   return SAIL_OK;
 }
@@ -1014,6 +1100,7 @@ int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, cons
   if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_render before sail_set_scene");
   if (spp < 0 || (spp > 0 && (!inv || !seeds)) || !eye || maxBounces < 0 || maxBounces > 1024)
     return fail(c, SAIL_E_INVALID, "sail_render_schedule: bad arguments (spp=%d bounces=%d)", spp, maxBounces);
+  if (int rc = flushQueued(c)) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   memcpy(c->eyeCache, eye, sizeof(float) * 3);
   c->hostSamples.clear();
@@ -1035,8 +1122,38 @@ int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, cons
   return SAIL_OK;
 }
 
+// One progressive sample (Renderer.render): queued, and launched with the samples queued after it once launchSpp of
+// them are waiting or anything observes or changes the context (flushQueued). The sample's record is built now,
+// from the sample index it is given now, exactly as sail_render_schedule builds it.
 int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed, int maxBounces) {
-  return sail_render_schedule(c, inv, &seed, eye, 1, maxBounces);
+  if (!c) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    for (sail_ctx* s : c->subs) if (int rc = sail_render(s, inv, eye, seed, maxBounces)) return relay(c, rc, s);
+    c->dirty = true;
+    return SAIL_OK;
+  }
+  if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_render before sail_set_scene");
+  if (!inv || !eye || maxBounces < 0 || maxBounces > 1024)
+    return fail(c, SAIL_E_INVALID, "sail_render: bad arguments (bounces=%d)", maxBounces);
+  // a launch has one eye (its pre-cull decisions) and one bounce count
+  if (!c->queued.empty() && (maxBounces != c->queuedBounces || memcmp(eye, c->eyeCache, sizeof(float) * 3) != 0))
+    if (int rc = flushQueued(c)) return rc;
+  memcpy(c->eyeCache, eye, sizeof(float) * 3);
+  c->queuedBounces = maxBounces;
+  const uint64_t k = c->k;
+  if (!(c->partMode == SAIL_PART_SAMPLES && c->world > 1 && (int)(k % (uint64_t)c->world) != c->rank)) {
+    SailSample S;
+    memset(&S, 0, sizeof S);
+    cornerDirs(inv, eye, S.d);
+    S.seed = seed;
+    S.mixw = (float)((double)k / (double)(k + 1));  // tracer.js:97, f64 then uniform1f
+    c->queued.push_back(S);
+    c->samplesThisRank++;
+  }
+  c->k++;
+  c->reduced = false;
+  if ((int)c->queued.size() >= c->launchSpp) return flushQueued(c);
+  return SAIL_OK;
 }
 
 int sail_reset(sail_ctx* c) {
@@ -1056,6 +1173,7 @@ int sail_sync(sail_ctx* c) {
     for (sail_ctx* s : c->subs) if (int rc = sail_sync(s)) return relay(c, rc, s);
     return groupCommCheck(c);
   }
+  if (int rc = flushQueued(c)) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = commCheck(c, c->comm)) return rc;
@@ -1222,6 +1340,7 @@ int sail_get_stats(sail_ctx* c, sail_stats* s) {
 int sail_accum_device_ptr(sail_ctx* c, void** ptr, size_t* bytes) {
   if (!c || !ptr || !bytes) return SAIL_E_INVALID;
   if (!c->subs.empty()) return relay(c, sail_accum_device_ptr(c->subs[0], ptr, bytes), c->subs[0]);
+  if (int rc = flushQueued(c)) return rc;  // the sums the caller's collective will read are queued on this stream
   *ptr = c->accum;
   *bytes = (size_t)c->W * c->H * sizeof(float4);
   return SAIL_OK;
@@ -1265,24 +1384,84 @@ int sail_reduce(sail_ctx* c, int root) {
   }
   if (!c->comm) return fail(c, SAIL_E_STATE, "sail_reduce before sail_comm_init");
   if (root < 0 || root >= c->commRanks) return fail(c, SAIL_E_INVALID, "sail_reduce: root %d of %d ranks", root, c->commRanks);
+  if (int rc = flushQueued(c)) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   const bool isRoot = c->commRank == root;
-  if (isRoot) { if (int rc = ensureFrame(c)) return rc; }
-  // out of place into root's frame: every reduce sums the ranks' cumulative accumulators afresh
-  const size_t count = (size_t)c->W * c->H * 4;
   const bool tiles = c->partMode == SAIL_PART_TILES;
+  const bool aov = c->aovN || c->aovP;
+  // a sample split shows the AOVs of the rank that rendered the last sample: the others send -0 maps
+  const bool own = tiles || c->rank == aovOwner(c->k, c->world);
+  if (isRoot || (aov && !own)) { if (int rc = ensureFrame(c)) return rc; }
+  const size_t np = (size_t)c->W * c->H, count = np * 4;
+  if (aov && !own) {
+    if (c->frameN) HIPCHK(c, fillNegZero(c->frameN, np, c->stream));
+    if (c->frameP) HIPCHK(c, fillNegZero(c->frameP, np, c->stream));
+  }
+  // out of place into root's frame: every reduce sums the ranks' cumulative accumulators afresh
+  float4* sendN = own ? c->aovN : c->frameN;
+  float4* sendP = own ? c->aovP : c->frameP;
   int r = g_rccl.groupStart();
   if (r == 0) r = g_rccl.reduce(c->accum, isRoot ? c->frame : c->accum, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
-  if (r == 0 && tiles && c->aovN) r = g_rccl.reduce(c->aovN, isRoot ? c->frameN : c->aovN, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
-  if (r == 0 && tiles && c->aovP) r = g_rccl.reduce(c->aovP, isRoot ? c->frameP : c->aovP, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  if (r == 0 && c->aovN) r = g_rccl.reduce(sendN, isRoot ? c->frameN : sendN, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
+  if (r == 0 && c->aovP) r = g_rccl.reduce(sendP, isRoot ? c->frameP : sendP, count, kNcclFloat32, kNcclSum, root, c->comm, c->stream);
   const int r2 = g_rccl.groupEnd();
   if (r || r2) return fail(c, SAIL_E_RCCL, "ncclReduce: %s", g_rccl.errStr ? g_rccl.errStr(r ? r : r2) : "?");
-  if (isRoot && !tiles) {  // a sample split shows root's own AOVs
-    if (c->aovN) HIPCHK(c, hipMemcpyAsync(c->frameN, c->aovN, count * 4, hipMemcpyDeviceToDevice, c->stream));
-    if (c->aovP) HIPCHK(c, hipMemcpyAsync(c->frameP, c->aovP, count * 4, hipMemcpyDeviceToDevice, c->stream));
-  }
   if (int rc = commCheck(c, c->comm)) return rc;
   c->reduced = isRoot;
+  return SAIL_OK;
+}
+
+// ---- checkpoint / resume --------------------------------------------------------------------------------------------
+int sail_accum_parts(sail_ctx* c, int* parts) {
+  if (!c || !parts) return SAIL_E_INVALID;
+  *parts = c->subs.empty() ? 1 : (int)c->subs.size();
+  return SAIL_OK;
+}
+
+int sail_save_accum(sail_ctx* c, int part, float* sums, uint64_t* k) {
+  if (!c || !sums || !k) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    if (part < 0 || part >= (int)c->subs.size()) return fail(c, SAIL_E_INVALID, "sail_save_accum: part %d of %d", part, (int)c->subs.size());
+    return relay(c, sail_save_accum(c->subs[part], 0, sums, k), c->subs[part]);
+  }
+  if (part != 0) return fail(c, SAIL_E_INVALID, "sail_save_accum: part %d of 1", part);
+  if (int rc = sail_sync(c)) return rc;
+  HIPCHK(c, hipMemcpy(sums, c->accum, (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
+  *k = c->k;
+  return SAIL_OK;
+}
+
+int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
+  if (!c || !sums || k > (1ull << 53)) return SAIL_E_INVALID;
+  if (!c->subs.empty()) {
+    const int nd = (int)c->subs.size();
+    if (part < -1 || part >= nd) return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d of %d", part, nd);
+    for (int i = 0; i < nd; i++) {  // part -1: each device keeps its share of the frame; else one part, every k
+      if (part == -1 || part == i) {
+        if (int rc = sail_load_accum(c->subs[i], part == -1 ? -1 : 0, sums, k)) return relay(c, rc, c->subs[i]);
+      } else {
+        c->subs[i]->k = k;
+      }
+    }
+    c->dirty = true;
+    return SAIL_OK;
+  }
+  if (part != 0 && part != -1) return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d of 1", part);
+  if (part == -1 && c->world > 1 && c->partMode == SAIL_PART_SAMPLES && c->accumMode != SAIL_ACCUM_SUM)
+    return fail(c, SAIL_E_INVALID, "sail_load_accum: a running mean cannot be split by samples");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = resetAccum(c)) return rc;  // queued samples, stats and AOVs restart; the accumulator is replaced
+  std::vector<float> mine;
+  const float* src = sums;
+  if (part == -1 && c->world > 1) { ownedPart(c, sums, mine); src = mine.data(); }
+  HIPCHK(c, hipMemcpyAsync(c->accum, src, (size_t)c->W * c->H * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->k = k;
+  // this rank's samples among 0 .. k-1 (every one, or those k' = rank mod world of a sample split)
+  if (c->partMode == SAIL_PART_SAMPLES && c->world > 1)
+    c->samplesThisRank = k > (uint64_t)c->rank ? (k - 1 - (uint64_t)c->rank) / (uint64_t)c->world + 1 : 0;
+  else
+    c->samplesThisRank = k;
   return SAIL_OK;
 }
 

@@ -281,6 +281,50 @@ napi_value ReadAccum(napi_env env, napi_callback_info info) {
   if (rc) return throwSail(env, "sail_read_accum", rc, h->ctx);
   return arr;
 }
+// checkpoint / resume (sail_accum_parts, sail_save_accum, sail_load_accum)
+napi_value SaveAccum(napi_env env, napi_callback_info info) {  // (ctx) -> {k, parts: [Float32Array]}
+  napi_value a[1];
+  if (!args(env, info, 1, a)) return nullptr;
+  Handle* h;
+  if (!getHandle(env, a[0], &h)) return nullptr;
+  int parts = 0;
+  int rc = sail_accum_parts(h->ctx, &parts);
+  if (rc) return throwSail(env, "sail_accum_parts", rc, h->ctx);
+  napi_value list, out;
+  NAPI_OK(napi_create_array_with_length(env, (size_t)parts, &list));
+  uint64_t k = 0;
+  for (int i = 0; i < parts; i++) {
+    void* p = nullptr;
+    napi_value arr = makeTyped(env, napi_float32_array, (size_t)h->W * h->H * 4, 4, &p);
+    rc = sail_save_accum(h->ctx, i, (float*)p, &k);
+    if (rc) return throwSail(env, "sail_save_accum", rc, h->ctx);
+    napi_set_element(env, list, (uint32_t)i, arr);
+  }
+  NAPI_OK(napi_create_object(env, &out));
+  napi_set_named_property(env, out, "k", num(env, (double)k));
+  napi_set_named_property(env, out, "parts", list);
+  return out;
+}
+napi_value LoadAccum(napi_env env, napi_callback_info info) {  // (ctx, part, Float32Array sums, k)
+  napi_value a[4];
+  if (!args(env, info, 4, a)) return nullptr;
+  Handle* h;
+  int part;
+  float* sums;
+  size_t n;
+  double k;
+  if (!getHandle(env, a[0], &h) || !getInt(env, a[1], &part) || !getArray(env, a[2], napi_float32_array, &sums, &n) ||
+      !getDouble(env, a[3], &k))
+    return nullptr;
+  if (n != (size_t)h->W * h->H * 4) { napi_throw_range_error(env, nullptr, "accumulator has the wrong size"); return nullptr; }
+  if (!(k >= 0.0 && k <= 9007199254740992.0) || k != (double)(uint64_t)k) {
+    napi_throw_range_error(env, nullptr, "sample index must be a non-negative integer");
+    return nullptr;
+  }
+  const int rc = sail_load_accum(h->ctx, part, sums, (uint64_t)k);
+  if (rc) return throwSail(env, "sail_load_accum", rc, h->ctx);
+  return undef(env);
+}
 napi_value Filter(napi_env env, napi_callback_info info) {  // (ctx, kind, weights|null, rx, ry, gamma) -> {rgba, rgba8}
   napi_value a[6];
   if (!args(env, info, 6, a)) return nullptr;
@@ -451,6 +495,8 @@ napi_value Init(napi_env env, napi_value exports) {
       {"sync", 0, Sync, 0, 0, 0, napi_enumerable, 0},
       {"readback", 0, Readback, 0, 0, 0, napi_enumerable, 0},
       {"readAccum", 0, ReadAccum, 0, 0, 0, napi_enumerable, 0},
+      {"saveAccum", 0, SaveAccum, 0, 0, 0, napi_enumerable, 0},
+      {"loadAccum", 0, LoadAccum, 0, 0, 0, napi_enumerable, 0},
       {"filter", 0, Filter, 0, 0, 0, napi_enumerable, 0},
       {"stats", 0, Stats, 0, 0, 0, napi_enumerable, 0},
       {"pick", 0, Pick, 0, 0, 0, napi_enumerable, 0},

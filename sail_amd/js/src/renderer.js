@@ -43,7 +43,13 @@ class Renderer {
     if (this.devices && this.devices.length < 1) throw new Error('Renderer: devices must name at least one GPU');
     this.maxBounces = opts.maxBounces || MAXBOUNCES;
     this.deterministic = !!opts.deterministic;  // frozen schedule (SURVEY §8(d)) instead of Math.random + clock
-    this.accumulation = opts.accumulation || 'mix';
+    // a sample split sums every device's own samples, so it accumulates sums (a running mean cannot be split)
+    this.accumulation = opts.accumulation || (opts.partition === 'samples' ? 'sum' : 'mix');
+    if (!(this.accumulation in ACCUM)) throw new Error(`Renderer: unknown accumulation '${this.accumulation}'`);
+    if (opts.partition !== undefined && opts.partition !== 'tiles' && opts.partition !== 'samples')
+      throw new Error(`Renderer: unknown partition '${opts.partition}' (tiles | samples)`);
+    if (opts.partition === 'samples' && this.accumulation !== 'sum' && this.devices && this.devices.length > 1)
+      throw new Error("Renderer: partition 'samples' needs accumulation 'sum' (a running mean cannot be split by samples)");
     this.aov = opts.aov !== false;
     this.display = opts.display === undefined ? !!this.canvas : !!opts.display;
     this.lib = native.load();
@@ -136,6 +142,20 @@ class Renderer {
   }
   // many rays at once: Float32Array of 6 floats per ray -> {index: Int32Array, t: Float32Array}
   pickRays(rays) { return this.lib.pick(this.ctx, rays); }
+
+  // checkpoint of a progressive render: {k: samples so far, parts: [Float32Array accumulator per device],
+  // width, height}; load() into a renderer of the same size, scene, devices and accumulation continues it bit for bit
+  save() {
+    const ck = this.lib.saveAccum(this.ctx);
+    return { k: ck.k, parts: ck.parts, width: this.width, height: this.height, accumulation: this.accumulation };
+  }
+  load(ckpt, scene) {
+    if (ckpt.width !== this.width || ckpt.height !== this.height) throw new Error('Renderer.load: checkpoint size differs');
+    if (ckpt.accumulation && ckpt.accumulation !== this.accumulation) throw new Error('Renderer.load: accumulation mode differs');
+    if (ckpt.frame) this.lib.loadAccum(this.ctx, -1, ckpt.frame, ckpt.k);
+    else ckpt.parts.forEach((p, i) => this.lib.loadAccum(this.ctx, i, p, ckpt.k));
+    if (scene) scene.sampleCount = ckpt.k;  // the next render() draws sample k (its jitter and seed)
+  }
 
   readPixels() { return this.lib.readback(this.ctx, false).rgba; }
   readAccum() { return this.lib.readAccum(this.ctx); }

@@ -4,12 +4,12 @@
 // one launch per call), and (b) with renderSamples(scene, spp) (one schedule, 32-sample launches).
 // Wall time is taken in JS around the calls and a readPixels() that waits for the device; the kernel time
 // comes from the library's HIP events (renderer.stats()).
-//   node sail_amd/js/tools/bench_host.js [--width 1920] [--height 1080] [--bounces 8] [--frames 256] [--spp 1024]
+//   node sail_amd/js/tools/bench_host.js [--width 1920] [--height 1080] [--bounces 8] [--frames 1024] [--spp 1024]
 const path = require('path');
 const Sail = require(path.join(__dirname, '..'));
 
 function args() {
-  const o = { width: 1920, height: 1080, bounces: 8, frames: 256, spp: 1024 };
+  const o = { width: 1920, height: 1080, bounces: 8, frames: 1024, spp: 1024 };
   const a = process.argv.slice(2);
   for (let i = 0; i < a.length; i += 2) o[a[i].replace(/^--/, '')] = parseInt(a[i + 1], 10);
   return o;

@@ -1,7 +1,7 @@
 'use strict';
 // Renders a frozen scene through Sail.Renderer -> N-API -> libsail_hip.so and writes the raw accumulator
 // (and the canvas pixels) for tests/test_js_host.py to compare with the CPU oracle. Needs an MI355X.
-// argv: scene W H spp bounces mode(sum|mix) api(samples|frames|progressive) out_prefix [filter [filter-r]]
+// argv: scene W H spp bounces mode(sum|mix) api(samples|frames|progressive|resume) out_prefix [filter [filter-r]]
 // env SAIL_TEST_DEVICES=0,0,0: a multi-device Renderer ({devices: [...]}); progressive = half the samples as
 // frames, a display pass (reduces the devices' frames), the other half, then the readback
 const fs = require('fs');
@@ -14,10 +14,20 @@ if (filter) {  // the reference's scene.filter = name; scene.filter.addParam('r'
   if (filterR) scene.filter.addParam('r', filterR);
 }
 const devices = process.env.SAIL_TEST_DEVICES ? process.env.SAIL_TEST_DEVICES.split(',').map(Number) : undefined;
-const r = new Sail.Renderer({ width: +W, height: +H, deterministic: true, accumulation: mode, maxBounces: +B, display: false,
-  devices });
+const opts = { width: +W, height: +H, deterministic: true, accumulation: mode, maxBounces: +B, display: false, devices };
+let r = new Sail.Renderer(opts);
 r.update(scene);
 if (api === 'samples') r.renderSamples(scene, +spp);
+else if (api === 'resume') {  // half the samples as frames, save(), a NEW renderer, load(), the other half
+  const half = Math.floor(+spp / 2);
+  for (let i = 0; i < half; i++) r.render(scene);
+  const ck = r.save();
+  r.destroy();
+  r = new Sail.Renderer(opts);
+  r.update(scene);
+  r.load(ck, scene);
+  for (let i = half; i < +spp; i++) r.render(scene);
+}
 else if (api === 'progressive') {
   const half = Math.floor(+spp / 2);
   for (let i = 0; i < half; i++) r.render(scene);

@@ -48,3 +48,47 @@ def test_gpus_beyond_visible_devices_fails():
     r = _bench(["--gpus", "64", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1"})
     assert r.returncode != 0 and "HIP devices are visible" in r.stderr
     assert r.stdout.strip() == ""
+
+
+class _FrameCtx:
+    """stands in for a context whose reduced frame is `acc` (bench.validate_frame reads it with read_accum)"""
+
+    def __init__(self, acc):
+        self.acc = acc
+
+    def read_accum(self):
+        return self.acc.copy()
+
+
+def test_validate_frame_refuses_a_broken_reduce(fixtures, capsys):
+    """bench.py checks the reduced frame after its timed steps: every count == spp and oracle crops in tiles of
+    several ranks; a reduce that drops or double-counts one rank's tiles ends the run (exit 3) with no number"""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle
+    from sail_amd import capi
+    sc = fixtures["scenes"]["C1"]
+    W, H, B, spp, ngpu = 130, 70, 3, 2, 4
+    masks = capi.plugin_masks(sc["plugins"])
+    mvp = np.array(sc["mvp_rowmajor"])
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    good = oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B)
+    rep = bench.validate_frame(_FrameCtx(good), sc, masks, mvp, W, H, B, spp, inv, seeds, capi.PART_TILES, ngpu)
+    assert rep["pixels_with_wrong_count"] == 0 and all(c["match"] for c in rep["oracle_crops"])
+    assert {c["rank"] for c in rep["oracle_crops"]} >= {0, 3}
+    for broken in ("dropped", "doubled", "wrong"):
+        acc = good.copy()
+        tile = acc[0:64, 64:128]  # tile 1 (rank 1 of 4)
+        if broken == "dropped":
+            tile[...] = 0.0
+        elif broken == "doubled":
+            tile[...] *= 2.0
+        else:  # counts right, radiance of rank 3's tile perturbed
+            acc[0:64, 0:64, 0] = np.nextafter(acc[0:64, 0:64, 0], np.float32(np.inf))
+            acc[64:70, 128:130, 0] += 1e-3
+        with pytest.raises(SystemExit) as e:
+            bench.validate_frame(_FrameCtx(acc), sc, masks, mvp, W, H, B, spp, inv, seeds, capi.PART_TILES, ngpu)
+        assert e.value.code == 3
+    out = capsys.readouterr()
+    assert out.out == "" and "failed validation" in out.err

@@ -36,14 +36,38 @@ def _sched(sc, W, H, k0, spp):
 
 CASES = [("C1", 64, 48, 8, 5), ("C1", 33, 17, 4, 8), ("C3", 40, 40, 4, 8), ("UI", 48, 48, 4, 5),
          ("ALL", 40, 32, 4, 6), ("C4", 32, 32, 2, 12), ("C1g", 16, 16, 2, 16)]
+# "rccl": the distinct-device branch (ncclCommInitAll + grouped ncclReduce into device 0) forced at one device by
+# SAIL_DEBUG_FORCE_RCCL; "all": every visible GPU as distinct devices (skipped below 2: the driver's 8-GPU node)
+RCCL1 = "rccl"
+ALL_GPUS = "all"
+
+
+def _devices(spec):
+    """a device list, a forced-RCCL one-device context, or every visible GPU"""
+    if spec == RCCL1:
+        return [0], {capi.DEBUG_FORCE_RCCL: 1}
+    if spec == ALL_GPUS:
+        n = capi.device_count()
+        if n < 2:
+            pytest.skip("distinct-device reduce needs at least 2 GPUs")
+        return list(range(n)), {}
+    return spec, {}
+
+
+def _ctx(W, H, spec, flags=0):
+    devices, dbg = _devices(spec)
+    ctx = capi.Context(W, H, devices=devices, flags=flags)
+    for opt, val in dbg.items():
+        ctx.set_debug(opt, val)
+    return ctx
 
 
 @pytest.mark.parametrize("name,W,H,spp,B", CASES)
-@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], RCCL1, ALL_GPUS])
 def test_multi_device_context_bit_exact(gpu, fixtures, name, W, H, spp, B, devices):
     sc = fixtures["scenes"][name]
     inv, seeds = _sched(sc, W, H, 0, spp)
-    ctx = capi.Context(W, H, devices=devices, flags=capi.FLAG_SEGMENT_COUNT | capi.FLAG_AOV)
+    ctx = _ctx(W, H, devices, flags=capi.FLAG_SEGMENT_COUNT | capi.FLAG_AOV)
     try:
         ctx.set_scene_dict(sc)
         ctx.set_launch_samples(3)
@@ -62,13 +86,14 @@ def test_multi_device_context_bit_exact(gpu, fixtures, name, W, H, spp, B, devic
 
 
 @pytest.mark.parametrize("mode", [capi.PART_TILES, capi.PART_SAMPLES])
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0]])
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0], RCCL1, ALL_GPUS])
 def test_progressive_reduces(gpu, fixtures, mode, devices):
-    """render k -> readback (reduce) -> render k -> readback equals the 2k-sample single-device frame"""
+    """render k -> readback (reduce) -> render k -> readback equals the 2k-sample single-device frame; the AOVs
+    shown are the last sample's (k = 3 per half: with 2 or 5 devices the last sample is not device 0's)"""
     sc = fixtures["scenes"]["C3"]
     W, H, B, k = 150, 70, 5, 3
     inv, seeds = _sched(sc, W, H, 0, 2 * k)
-    ctx = capi.Context(W, H, devices=devices, flags=capi.FLAG_AOV)
+    ctx = _ctx(W, H, devices, flags=capi.FLAG_AOV)
     try:
         ctx.set_scene_dict(sc)
         ctx.set_partition(0, 1, mode)
@@ -78,6 +103,7 @@ def test_progressive_reduces(gpu, fixtures, mode, devices):
         got = ctx.read_accum()
         again = ctx.read_accum()          # no render in between: the same frame
         _, gn, gp = ctx.readback(aov=True)
+        ndev = len(_devices(devices)[0])
     finally:
         ctx.close()
     masks = capi.plugin_masks(sc["plugins"])
@@ -85,10 +111,10 @@ def test_progressive_reduces(gpu, fixtures, mode, devices):
     want, wn, wp = oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, aov=True)
     assert bit_equal(got, again).all()
     assert (got[..., 3] == 2 * k).all(), "every pixel counts each sample once"
-    if mode == capi.PART_TILES or len(devices) == 1:
+    assert bit_equal(gn, wn).all() and bit_equal(gp, wp).all()  # the last sample's AOVs, whoever rendered it
+    if mode == capi.PART_TILES or ndev == 1:
         assert bit_equal(first, want_k).all()
         assert bit_equal(got, want).all()
-        assert bit_equal(gn, wn).all() and bit_equal(gp, wp).all()
     else:  # the same samples summed in rank order: equal to rounding
         assert np.allclose(first, want_k, rtol=1e-5, atol=1e-5)
         assert np.allclose(got, want, rtol=1e-5, atol=1e-5)
@@ -130,20 +156,29 @@ def test_multi_device_rejects_running_mean_sample_split(gpu, fixtures):
 @pytest.mark.parametrize("kind,fname,r", [(capi.FILTER_WINDOW, "gaussian", (1.5, 2.5)),
                                           (capi.FILTER_WAVELET, None, (2.0, 2.0)),
                                           (capi.FILTER_TONEMAPPING, None, (0.0, 0.0))])
-def test_multi_device_display_filter(gpu, fixtures, kind, fname, r):
-    """Renderer.image() on a multi-device context: the filter runs on device 0 over the reduced frame"""
+@pytest.mark.parametrize("mode,devices", [(capi.PART_TILES, [0, 0, 0]), (capi.PART_SAMPLES, [0, 0, 0]),
+                                          (capi.PART_SAMPLES, RCCL1)])
+def test_multi_device_display_filter(gpu, fixtures, kind, fname, r, mode, devices):
+    """Renderer.image() on a multi-device context: the filter runs on device 0 over the reduced frame; with a
+    sample split (spp 5 on 3 devices: the last sample is device 1's) the wavelet reads that sample's AOVs"""
     sc = fixtures["scenes"]["C3"]
-    W, H, B, spp = 140, 72, 5, 3
+    W, H, B, spp = 140, 72, 5, 5
     inv, seeds = _sched(sc, W, H, 0, spp)
     w = np.array([float(x) for x in fixtures["filters"][fname]["weight_text"]], np.float32) if fname else None
-    ctx = capi.Context(W, H, devices=[0, 0, 0], flags=capi.FLAG_AOV)
+    ctx = _ctx(W, H, devices, flags=capi.FLAG_AOV)
     try:
         ctx.set_scene_dict(sc)
+        ctx.set_partition(0, 1, mode)
         ctx.render_schedule(inv, seeds, sc["eye"], B)
+        acc = ctx.read_accum()
         got = ctx.filter(kind, w, r[0], r[1], 2.2)
     finally:
         ctx.close()
-    acc, n, p = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B, aov=True)
+    want_acc, n, p = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B, aov=True)
+    if mode == capi.PART_TILES or devices == RCCL1:
+        assert bit_equal(acc, want_acc).all()
+    else:  # the filters read the frame the devices summed (rank order)
+        assert np.allclose(acc, want_acc, rtol=1e-5, atol=1e-5)
     mean = acc.copy()
     mean[..., :3] = acc[..., :3] / acc[..., 3:4]
     mean[..., 3] = 1.0

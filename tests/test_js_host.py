@@ -76,6 +76,18 @@ def test_renderer_fails_loudly_without_device():
     assert r.returncode != 0 and ("no HIP device" in r.stderr or "not built" in r.stderr)
 
 
+def test_renderer_rejects_running_mean_sample_split():
+    """partition 'samples' over several devices needs sums; it defaults to them, and an explicit running mean is
+    refused before any device is touched"""
+    code = ("const S=require('./sail_amd/js'); try { new S.Renderer({width:8,height:8,devices:[0,0],"
+            "partition:'samples',accumulation:'mix'}); console.log('created') } catch (e) { console.log(e.message) }")
+    out = subprocess.run([NODE, "-e", code], cwd=ROOT, capture_output=True, text=True, check=True).stdout
+    assert "needs accumulation 'sum'" in out
+    code = "const S=require('./sail_amd/js'); try { new S.Renderer({width:8,height:8,partition:'rows'}) } catch (e) { console.log(e.message) }"
+    out = subprocess.run([NODE, "-e", code], cwd=ROOT, capture_output=True, text=True, check=True).stdout
+    assert "unknown partition" in out
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,W,H,spp,B,mode,api,devices", [
     ("C1", 40, 30, 4, 5, "sum", "samples", None),
@@ -86,6 +98,9 @@ def test_renderer_fails_loudly_without_device():
     ("C1", 150, 70, 4, 5, "sum", "progressive", "0"),
     ("C3", 150, 70, 4, 5, "sum", "progressive", "0,0,0"),
     ("UI", 130, 66, 4, 5, "mix", "progressive", "0,0"),
+    # renderer.save() -> a new Renderer -> load() -> the remaining frames (checkpoint / resume)
+    ("C3", 150, 70, 6, 5, "sum", "resume", None),
+    ("C1", 150, 70, 5, 5, "mix", "resume", "0,0,0"),
 ])
 def test_js_renderer_bit_exact_vs_oracle(tmp_path, fixtures, exported, name, W, H, spp, B, mode, api, devices):
     if capi.device_count() < 1:
