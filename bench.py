@@ -41,7 +41,7 @@ CONFIGS = {
 CONFIG = CONFIGS["C2"]
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
-VALU_CLOCK_HZ = 2.4e9      # MI355X peak engine clock, if the device does not report one
+VALU_ISSUE_CEILING = 0.42  # plain v_fma/mul/add_f32 wave-instructions per SIMD-cycle under load (tools/pk_probe.hip, profiles/r02_pk_probe.json)
 
 
 def load_scene(name="C1"):
@@ -130,7 +130,9 @@ def cpu_baseline(sc, masks, mvp, W, H, B, budget_s=10.0):
 
 
 def ops_per_segment(sc, masks, mvp, W, H, B):
-    """Algorithmic f32 ops per segment from the op-counting oracle build (SURVEY §8(d) op model)."""
+    """Algorithmic f32 ops per segment from the op-counting oracle build (SURVEY §8(d) op model): (every op of the
+    reference program, the live-op model without the last bounce's dead ops -- its throughput update, next ray,
+    BSDF sample and material weight, which no output reads)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle
     inv, seeds = capi.schedule(mvp, W, H, 0, 2)
@@ -140,7 +142,7 @@ def ops_per_segment(sc, masks, mvp, W, H, B):
     oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=((W - cw) // 2, (H - ch) // 2, cw, ch),
                   accum=acc, count=True)
     segs, ops = oracle.counters(count=True)
-    return ops / max(segs, 1)
+    return ops / max(segs, 1), oracle.ops_live() / max(segs, 1)
 
 
 def profiled_traffic(workload, px, spp, bounces):
@@ -157,19 +159,21 @@ def profiled_traffic(workload, px, spp, bounces):
 
 
 def valu_issue(pmc, avg_launch_s, device):
-    """Executed wave64 VALU instructions per launch (PMC SQ_INSTS_VALU, the same committed summary as
-    `traffic`) per second of the live launch time, against one wave64 VALU issue per SIMD every 2 cycles
-    (v_fma_f32 throughput, MI355X_MICROARCH.md) at the device's peak engine clock: how busy the vector pipe is,
-    as opposed to the algorithmic-op fraction above (f64 and transcendental instructions take 4-8 cycles,
-    so this understates the pipe's occupancy)."""
+    """Executed wave64 VALU instructions per launch (PMC SQ_INSTS_VALU, the same committed summary as `traffic`)
+    per SIMD-cycle of the live launch at the engine clock the PMC pass measured (GRBM_GUI_ACTIVE / 8 XCDs / the
+    dispatch's own duration, tools/pmc_summary.py), beside the plain-f32 issue ceiling tools/pk_probe.hip measured
+    under load (0.42 wave-instructions per SIMD-cycle): how busy the vector pipe is, as opposed to the
+    algorithmic-op fraction (f64 and transcendental instructions take 4-8 cycles, so this understates it)."""
     if not pmc or "SQ_INSTS_VALU" not in pmc.get("sq", {}):
         return None
-    cus, clock = capi.device_info(device)
-    clock = clock if clock > 0 else VALU_CLOCK_HZ
-    peak = cus * 4 * clock / 2
-    achieved = pmc["sq"]["SQ_INSTS_VALU"] / avg_launch_s
-    return {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1), "unit": "G wave-instr/s",
-            "frac": round(achieved / peak, 4), "lane_utilisation": round(pmc.get("derived", {}).get("valu_lane_utilisation", 0.0), 3)}
+    cus, _ = capi.device_info(device)
+    clk = pmc.get("derived", {}).get("effective_clock_hz")
+    if not clk:
+        return None
+    per_cycle = pmc["sq"]["SQ_INSTS_VALU"] / (avg_launch_s * clk * cus * 4)
+    return {"per_simd_cycle": round(per_cycle, 4), "clock_ghz": round(clk / 1e9, 3), "ceiling_per_simd_cycle": VALU_ISSUE_CEILING,
+            "frac_of_ceiling": round(per_cycle / VALU_ISSUE_CEILING, 4), "clock_source": "PMC GRBM_GUI_ACTIVE / 8 / dispatch duration",
+            "lane_utilisation": round(pmc.get("derived", {}).get("valu_lane_utilisation", 0.0), 3)}
 
 
 def validate_frame(ctx, sc, masks, mvp, W, H, B, spp, inv, seeds, part, ngpu):
@@ -351,8 +355,9 @@ def main():
             for t in range(0, tx * ty, ngpu):
                 tiles_px += min(64, W - (t % tx) * 64) * min(64, H - (t // tx) * 64)
         segs_per_launch = tiles_px * args.launch_spp * B
-        ops_seg = ops_per_segment(sc, masks, mvp, W, H, B)
+        ops_seg, ops_live = ops_per_segment(sc, masks, mvp, W, H, B)
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
+        achieved_live = ops_live * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
         traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B)
         rec = {
@@ -379,7 +384,12 @@ def main():
                 # the op model counts every add/mul/min/max/divide/transcendental as one op: its ceiling is one op
                 # per lane per cycle (the FP32 peak above counts an FMA as two), so this is the pipe's fraction
                 "frac_one_op_per_lane": round(achieved_tflops / (FP32_PEAK_TFLOPS / 2), 4),
-                "ops_per_segment": round(ops_seg, 2), "kernel": ctx.kernel_name(),
+                "ops_per_segment": round(ops_seg, 2),
+                # the live-op model: the last bounce's dead ops (throughput, next ray, BSDF sample) left out
+                "ops_per_segment_live": round(ops_live, 2), "achieved_live": round(achieved_live, 3),
+                "frac_live": round(achieved_live / FP32_PEAK_TFLOPS, 4),
+                "formula": "ops_per_segment x pixels x launch_spp x bounces / avg_launch_s / 157.3e12",
+                "kernel": ctx.kernel_name(),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},

@@ -1197,6 +1197,35 @@ static V3 shade(const Intersect& ins, V3 wo, V3& wi, V3& fpdf) {  // :1-14
   return ins.emission + direct;
 }
 static unsigned long long g_segments = 0;
+#ifdef SAIL_COUNT_OPS
+// Live-op model (op-counting build only): after a path's last bounce only its radiance is read, so that bounce's
+// throughput update, next ray, BSDF sample and material weight are dead. Its live ops are the radiance update
+// e += (emission + direct) * fpdf and, on a lit matte surface, f (Lambert: (kd sc) / pi; Oren-Nayar: the shading
+// frame, the hash and the cosine sample it needs) and the light sample with its shadow ray when the scene has
+// lights. g_opsLastFull counts what the reference program does at the last bounce, g_opsLastLive the live part.
+static unsigned long long g_opsLastFull = 0, g_opsLastLive = 0;
+static void countLiveLast(const Intersect& ins, V3 woWorld, V3 fpdf) {
+  V3 direct = BLACKv;
+  if (veq(ins.emission, BLACKv) && ins.matCategory == MATTE && ((C.matMask >> MATTE) & 1u)) {
+    const Tex& tp = C.texParams;
+    const F kd = readFloat(tp, 1.0f, ins.matIndex, kTexLen), sigma = readFloat(tp, 2.0f, ins.matIndex, kTexLen);
+    V3 f;
+    if (sigma < F(kEps)) {
+      f = (kd * ins.sc) * F(kInvPI);
+    } else {
+      const F A = readFloat(tp, 3.0f, ins.matIndex, kTexLen), B = readFloat(tp, 4.0f, ins.matIndex, kTexLen);
+      const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
+      const V3 wo = worldToLocal(woWorld, ins.normal, ss, ts);
+      const V3 wi = cosineSampleHemisphere(random2(ins.seed));
+      f = orenNayar_f(kd * ins.sc, A, B, wo, wi);
+    }
+    if (C.ln > 0 && C.lightMask != 0u) direct = direct + light_sample(ins) * f;
+  }
+  const V3 e = (ins.emission + direct) * fpdf;
+  (void)e;
+  OPC(3);  // the e + ... sum
+}
+#endif
 static void trace(Ray ray, int maxDepth, V3& e, V3& n, V3& p) {  // :16-38
   V3 fpdf = WHITEv;
   e = BLACKv;
@@ -1207,12 +1236,24 @@ static void trace(Ray ray, int maxDepth, V3& e, V3& n, V3& p) {  // :16-38
     ins.seed = C.timeSinceStart + F((float)depth);
     if (ins.d >= F(kMaxDistance)) break;
     if (depth == 1) { n = ins.normal; p = ins.hit; }
+#ifdef SAIL_COUNT_OPS
+    const bool last = depth == maxDepth;
+    const unsigned long long before = g_ops;
+    if (last) {  // count the live part on its own, then the reference's full bounce as usual
+      countLiveLast(ins, -ray.dir, fpdf);
+      g_opsLastLive += g_ops - before;
+      g_ops = before;
+    }
+#endif
     V3 wi, _fpdf;
     e = e + shade(ins, -ray.dir, wi, _fpdf) * fpdf;
     fpdf = fpdf * _fpdf;
     const F outdot = dot(ins.normal, wi);
     ray.origin = ins.hit + ins.normal * (outdot > F(kEps) ? F(0.0001f) : F(-0.0001f));
     ray.dir = wi;
+#ifdef SAIL_COUNT_OPS
+    if (last) g_opsLastFull += g_ops - before;
+#endif
   }
 }
 
@@ -1302,6 +1343,16 @@ void oracle_reset_counters(void) {
   g_segments = 0;
 #ifdef SAIL_COUNT_OPS
   g_ops = 0;
+  g_opsLastFull = 0;
+  g_opsLastLive = 0;
+#endif
+}
+// ops of the live-op model: every op but the last bounce's dead ones (countLiveLast)
+unsigned long long oracle_ops_live(void) {
+#ifdef SAIL_COUNT_OPS
+  return g_ops - g_opsLastFull + g_opsLastLive;
+#else
+  return 0;
 #endif
 }
 unsigned long long oracle_ops(void) {

@@ -52,6 +52,7 @@ def lib(count: bool = False) -> ctypes.CDLL:
     L.oracle_intersect_t.argtypes = [f32p, ci, f32p, ci, u32, f32p, f32p]
     L.oracle_segments.restype = ctypes.c_ulonglong
     L.oracle_ops.restype = ctypes.c_ulonglong
+    L.oracle_ops_live.restype = ctypes.c_ulonglong
     L.oracle_reset_counters.restype = None
     _libs[key] = L
     return L
@@ -141,6 +142,11 @@ def intersect_t(objects, n, texparams, tn, shape_mask, o, d) -> float:
 def counters(count: bool = False):
     L = lib(count)
     return int(L.oracle_segments()), int(L.oracle_ops())
+
+
+def ops_live(count: bool = True) -> int:
+    """ops of the live-op model (the last bounce's dead ops left out; the counting build only)"""
+    return int(lib(count).oracle_ops_live())
 
 
 def reset_counters(count: bool = False):

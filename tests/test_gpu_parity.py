@@ -385,13 +385,17 @@ def test_odd_category_words(gpu, fixtures):
 
 
 # ---- one sample per call (Renderer.render): the sample-record ring wraps after 4096 calls ---------------------------
-def test_single_sample_frames_ring_wrap(gpu, fixtures):
+@pytest.mark.parametrize("launch_spp", [1, 32])
+def test_single_sample_frames_ring_wrap(gpu, fixtures, launch_spp):
+    """4,100 one-sample frames across the wrap of the 4,096-record sample ring: one launch per frame (launch_spp 1)
+    or queued 32 to a launch (sail_render's batching); the same frame either way"""
     sc = fixtures["scenes"]["C1"]
     W, H, B, spp = 8, 6, 4, 4100
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
     ctx = capi.Context(W, H, flags=capi.FLAG_SEGMENT_COUNT)
     try:
         ctx.set_scene_dict(sc)
+        ctx.set_launch_samples(launch_spp)
         for k in range(spp):
             ctx.render(inv[k], sc["eye"], float(seeds[k]), B)
         got = ctx.read_accum()
@@ -402,7 +406,7 @@ def test_single_sample_frames_ring_wrap(gpu, fixtures):
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
     segs, _ = oracle.counters()
     assert bit_equal(got, want).all()
-    assert st.segments == segs and st.launches == spp
+    assert st.segments == segs and st.launches == (spp + launch_spp - 1) // launch_spp
 
 
 # ---- degenerate rays through the division spec's fallback paths: exactly axis-aligned directions (zero and

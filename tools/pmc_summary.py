@@ -15,13 +15,19 @@ import sys
 
 
 def load(pdir, name):
+    """counter means over the trace-kernel dispatches of one pass, the kernels they were, and their mean duration
+    (the counter CSV's own Start/End timestamps, ns): every summary states what it profiled and for how long"""
     path = os.path.join(pdir, name, "run_counter_collection.csv")
     agg = collections.defaultdict(list)
+    disp = {}
     with open(path) as f:
         for r in csv.DictReader(f):
             if "sail_trace_kernel" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+                disp[r["Dispatch_Id"]] = (r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    kernels = sorted({k for k, _ in disp.values()})
+    dur = sum(d for _, d in disp.values()) / max(len(disp), 1)
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {"kernels": kernels, "dispatches": len(disp), "mean_ns": dur}
 
 
 def main():
@@ -31,16 +37,21 @@ def main():
     bounces = int(sys.argv[5]) if len(sys.argv) > 5 else 8
     workload = sys.argv[6] if len(sys.argv) > 6 else "cornell_box_readme_C2"
     c = {}
+    passes = {}
     for p in ("fetch", "write", "sq", "sq2"):
         if os.path.isdir(os.path.join(pdir, p)):
-            c.update(load(pdir, p)[0])
+            vals, meta = load(pdir, p)
+            c.update(vals)
+            passes[p] = meta
+    kernels = sorted({k for m in passes.values() for k in m["kernels"]})
     fetch_b = c["FETCH_SIZE"] * 1024 * 2
     write_b = c["WRITE_SIZE"] * 1024
     alg = px * 32
     waves = c.get("SQ_WAVES", 0)
     segs = px * spp * bounces
     rec = {
-        "kernel": "sail_trace_kernel", "workload": workload, "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
+        "kernel": kernels[0] if len(kernels) == 1 else kernels, "workload": workload,
+        "passes": passes, "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
         "hbm": {"fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
                 "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,
                 "raw_FETCH_SIZE_KiB": c["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": c["WRITE_SIZE"]},
@@ -55,6 +66,13 @@ def main():
             "vmem_writes_per_wave": c.get("SQ_INSTS_VMEM_WR", 0) / waves,
             "vmem_reads_per_segment_lane": c.get("SQ_INSTS_VMEM_RD", 0) * 64 / segs,
         }
+        sq = passes.get("sq")
+        if sq and sq["mean_ns"] > 0 and "GRBM_GUI_ACTIVE" in c:
+            # GRBM_GUI_ACTIVE counts GPU-busy cycles on each of the 8 XCDs: over the dispatch's own duration it is the
+            # engine clock the kernel ran at; VALU wave-instructions per SIMD (1,024 of them) per such cycle
+            clk = c["GRBM_GUI_ACTIVE"] / 8 / (sq["mean_ns"] * 1e-9)
+            rec["derived"]["effective_clock_hz"] = clk
+            rec["derived"]["valu_issue_per_simd_cycle"] = c["SQ_INSTS_VALU"] / (sq["mean_ns"] * 1e-9 * clk * 1024)
         if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
             # lanes doing work per VALU cycle; 1.0 = no divergence or masked lanes
             rec["derived"]["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64)
