@@ -16,6 +16,7 @@ import re
 import numpy as np
 import pytest
 
+import literal_pins as lp
 import oracle
 from sail_amd import capi
 
@@ -166,14 +167,7 @@ def _float_literals(text):
     return vals
 
 
-# functions of the generated program that no path of the trace runs (SURVEY §8(a) "Not on the hot path"):
-# never called, or only reachable through Beckmann (never selected), transmission BxDFs nobody builds, noise
-DEAD_FUNCTIONS = {
-    "noise", "fbm", "turbulence", "Grad", "fade", "lerp", "beckmann_d", "beckmann_pdf", "beckmann_sample_wh",
-    "lambertian_t_f", "lambertian_t_pdf", "lambertian_t_sample_f", "specular_t_f", "specular_t_pdf",
-    "specular_t_sample_f", "cosDPhi", "tanTheta", "random", "cosineSampleHemisphere2", "uniformSampleDisk",
-    "uniformSampleCone", "uniformSampleTriangle", "ortho", "modMatrix", "readVec2",
-}
+DEAD_FUNCTIONS = lp.DEAD_FUNCTIONS
 
 
 @pytest.mark.parametrize("name", ["C1", "C3", "C4", "ALL"])
@@ -214,28 +208,53 @@ def test_program_defines_match_kernel_and_oracle(fixtures, name):
     assert "v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)" in kern
 
 
-@pytest.mark.parametrize("name", ["C1", "C3", "C4", "ALL"])
-def test_program_literals_in_kernel_and_oracle(fixtures, name):
-    """every floating literal of every live function of the generated program is a constant of the HIP kernel
-    and of the oracle (as the same f32), or folded into a named per-scene host constant listed here"""
+def _literal_map():
+    with open(os.path.join(ROOT, "tests", "golden", "literal_map.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", list(lp.SCENES))
+def test_program_literals_mapped_to_their_functions(fixtures, name):
+    """every floating literal of every live function of the generated program has an entry in the committed table
+    tests/golden/literal_map.json (data: GLSL function -> literal -> the kernel function and the oracle function
+    that use it), and each entry holds in today's sources: the same f32 constant inside that function's body, or,
+    for the texture-row readers, the same column of the decoded row. Folded literals state the exact rewrite."""
     lits = fixtures["program_constants"][name]["literals"]
-    kern, orc = _float_literals(_src(KERNEL_SOURCES)), _float_literals(_src(ORACLE_SOURCES))
-    live = {fn: v for fn, v in lits.items() if fn not in DEAD_FUNCTIONS}
+    table = _literal_map()
+    live = {fn: v for fn, v in lits.items() if fn not in lp.DEAD_FUNCTIONS}
     assert len(live) > 20
-    missing = []
+    problems = []
     for fn, vals in sorted(live.items()):
         for v in vals:
-            if (fn, v) in GENERALISED:
+            if (fn, v) in lp.GENERALISED:
                 continue
-            b = np.float32(float(v)).view(np.uint32).item()
-            if b not in kern or b not in orc:
-                missing.append((fn, v, b in kern, b in orc))
-    assert not missing, missing
+            e = table.get(fn, {}).get(v)
+            if e is None:
+                problems.append((fn, v, "not in literal_map.json"))
+                continue
+            if e["kind"] == "folded":
+                if (fn, v) not in lp.FOLDED:
+                    problems.append((fn, v, "folded without a recorded reason"))
+                continue
+            for side in ("kernel", "oracle"):
+                path, func = e[side].rsplit(":", 1)
+                if not lp.literal_in_function(path, func, v, e["kind"]):
+                    problems.append((fn, v, side, e[side]))
+    assert not problems, problems
 
 
-# literals the build replaces on purpose
-GENERALISED = {
-    # fstrace.glsl main: the previous frame is read at gl_FragCoord.xy / 512.0 (the fixed 512 x 512 canvas,
-    # webgl.js:24); the build renders W x H and each pixel owns its accumulator, so the kernel has no such read
-    ("main", "512.0"),
-}
+def test_literal_map_is_not_vacuous():
+    """the table names real functions, and its float entries are specific: a changed constant breaks the pin"""
+    table = _literal_map()
+    funcs = {e[s] for ent in table.values() for e in ent.values() if e["kind"] != "folded" for s in ("kernel", "oracle")}
+    for f in funcs:
+        path, name = f.rsplit(":", 1)
+        assert lp.function_bodies(path, name), f
+    # the hash constants sit in the hash functions of both implementations, not anywhere in the sources
+    for v in ("12.9898", "78.233", "151.7182", "43758.5453", "63.7264", "10.873", "623.6736"):
+        e = table["random2"][v]
+        assert e["kernel"].endswith(":hash1") or e["kernel"].endswith(":random2"), e
+        assert e["oracle"].endswith(":hash1") or e["oracle"].endswith(":random2"), e
+    assert not lp.literal_in_function("sail_amd/csrc/sail_trace.hip", "hash1", "12.9897", "value")
+    assert table["equalZero"]["1e-3"]["kernel"].endswith(":equalZero")
+    assert table["point_sample"]["0.1"]["kernel"].endswith(":lightPrep")

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Per-rank trace throughput for world sizes 1/2/4/8 emulated on one GPU (rank 0's tiles only, no collective):
-predicts the strong-scaling efficiency of bench.py --gpus N before the reduce is added.
-Usage: tools/scaling_probe.py [config] [spp]"""
+"""Per-rank trace throughput for world sizes 1/2/4/8 emulated on one GPU (rank 0's and rank N-1's share only, no
+collective): predicts the strong-scaling efficiency of bench.py --gpus N before the reduce is added. A tile config
+renders the rank's tiles; a sample-split config (C5) renders its samples k = rank mod N of the whole frame.
+Usage: tools/scaling_probe.py [config] [spp] [--groups g] [--worlds 1,2,4,8]
+--groups g fixes the sample-group count (SAIL_DEBUG_SAMPLE_GROUPS) instead of the host's occupancy rule."""
+import argparse
 import json
 import os
 import sys
@@ -14,33 +17,55 @@ from sail_amd import capi  # noqa: E402
 
 
 def main():
-    cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "C2"]
-    spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", nargs="?", default="C2")
+    ap.add_argument("spp", nargs="?", type=int, default=256)
+    ap.add_argument("--groups", type=int, default=0)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    spp = a.spp
     W, H, B = cfg["width"], cfg["height"], cfg["bounces"]
+    part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
     sc = bench.load_scene(cfg["scene"])
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
     inv, seeds = capi.schedule(mvp, W, H, 0, spp)
     base = None
-    for world in (1, 2, 4, 8):
+    for world in (int(w) for w in a.worlds.split(",")):
         for rank in ([0, world - 1] if world > 1 else [0]):
             ctx = capi.Context(W, H)
+            if a.groups:
+                ctx.set_debug(capi.DEBUG_SAMPLE_GROUPS, a.groups)
             ctx.set_scene_dict(sc)
-            ctx.set_partition(rank, world, capi.PART_TILES)
+            ctx.set_partition(rank, world, part)
             ctx.render_schedule(inv[:32], seeds[:32], sc["eye"], B)  # warm-up
             ctx.sync()
-            ctx.reset()
-            t0 = time.perf_counter()
-            ctx.render_schedule(inv, seeds, sc["eye"], B)
-            ctx.sync()
-            dt = time.perf_counter() - t0
-            px = int(sum(int(w) * int(h) for _, _, w, h in capi.partition_tiles(W, H, rank, world)))
-            rate = px * spp * B / dt / 1e9
+            best = 1e30
+            for _ in range(a.reps):
+                ctx.reset()
+                t0 = time.perf_counter()
+                ctx.render_schedule(inv, seeds, sc["eye"], B)
+                ctx.sync()
+                best = min(best, time.perf_counter() - t0)
+            st = ctx.stats()
             ctx.close()
+            if part == capi.PART_TILES:
+                px = int(sum(int(w) * int(h) for _, _, w, h in capi.partition_tiles(W, H, rank, world)))
+                work = px * spp * B
+                share = px / (W * H)
+            else:
+                mine = len(range(rank, spp, world))
+                work = W * H * mine * B
+                share = mine / spp
+            rate = work / best / 1e9
             if base is None:
                 base = rate
-            print(json.dumps({"world": world, "rank": rank, "pixels": px, "s": round(dt, 4),
+            print(json.dumps({"config": a.config, "partition": "tiles" if part == capi.PART_TILES else "samples",
+                              "spp": spp, "groups": a.groups or "auto", "world": world, "rank": rank,
+                              "share": round(share, 5), "s": round(best, 4), "launches": int(st.launches),
                               "Gseg_per_s_per_gpu": round(rate, 3), "vs_1gpu": round(rate / base, 3),
-                              "frame_speedup_if_all_ranks_like_this": round(W * H / px * rate / base, 2)}), flush=True)
+                              "frame_speedup_if_all_ranks_like_this": round(rate / base / share, 2)}), flush=True)
 
 
 if __name__ == "__main__":
