@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc_mix.sh's two rocprofv3 passes (VALU instruction classes) for the trace kernel into one JSON:
+the counters per dispatch (mean), the kernel they came from, and each class per segment-lane (64 x counter /
+nominal segments of the launch) beside the algorithmic op count, so the executed/algorithmic inflation is attributed.
+Usage: tools/pmc_mix_summary.py gpurun_out/pmc_mix out.json launch_pixels launch_spp bounces workload [ops_per_segment]"""
+import collections
+import csv
+import json
+import os
+import sys
+
+CLASSES = ["SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32",
+           "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
+           "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"]
+
+
+def load(path):
+    agg = collections.defaultdict(list)
+    kernels, disp = set(), {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "sail_trace_kernel" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                kernels.add(r["Kernel_Name"])
+                disp[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return {k: sum(v) / len(v) for k, v in agg.items()}, kernels, sum(disp.values()) / max(len(disp), 1)
+
+
+def main():
+    pdir, out = sys.argv[1], sys.argv[2]
+    px, spp, bounces, workload = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
+    ops = float(sys.argv[7]) if len(sys.argv) > 7 else None
+    c, kernels, durs = {}, set(), {}
+    for p in ("mix1", "mix2"):
+        vals, ks, d = load(os.path.join(pdir, p, "run_counter_collection.csv"))
+        c.update(vals)
+        kernels |= ks
+        durs[p] = d
+    segs = px * spp * bounces
+    per = {k.replace("SQ_INSTS_VALU_", "").lower(): c[k] * 64 / segs for k in CLASSES if k in c}
+    total = c["SQ_INSTS_VALU"] * 64 / segs
+    per["other (moves, selects, compares, min/max, bit ops, lane ops)"] = total - sum(per.values())
+    rec = {"kernel": sorted(kernels)[0] if len(kernels) == 1 else sorted(kernels), "workload": workload,
+           "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
+           "source": "tools/pmc_mix.sh (rocprofv3 --pmc, two passes, kernel-trace only), mean per dispatch",
+           "dispatch_mean_ns": durs, "counters": c,
+           "valu_per_segment_lane": {"total": total, "by_class": per}}
+    if ops:
+        rec["valu_per_segment_lane"]["algorithmic_ops_per_segment"] = ops
+        rec["valu_per_segment_lane"]["inflation"] = total / ops
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec["valu_per_segment_lane"], indent=1))
+
+
+if __name__ == "__main__":
+    main()
