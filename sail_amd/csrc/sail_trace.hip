@@ -1546,11 +1546,13 @@ D void accumulateSample(float4& acc, V3 e, const SailSample& S, int mode) {
 // launches (one workgroup per block, every sample) are a separate compile-time instance, so they carry none of
 // the group bookkeeping in registers (sample groups add VGPR/SGPR spills to the flat kernels otherwise).
 struct TileWork { int ownedTile, sub, kBeg, kEnd, bid; };
-template <bool GROUPED>
+// NT-thread workgroups cover 16 x NT/16 pixel blocks, 4096 / NT of them per 64x64 tile
+template <bool GROUPED, int NT = 256>
 D TileWork tileWork(const SailTraceArgs& A) {
+  constexpr int kPer = 4096 / NT;
   TileWork w;
   if (GROUPED) {
-    const int nb = A.ownedTiles * 16;
+    const int nb = A.ownedTiles * kPer;
     const int bid = (int)blockIdx.x % nb, group = (int)blockIdx.x / nb;
     w.bid = bid;
     w.kBeg = group * A.groupSpp;
@@ -1560,12 +1562,23 @@ D TileWork tileWork(const SailTraceArgs& A) {
     w.kBeg = 0;
     w.kEnd = A.spp;
   }
-  w.ownedTile = w.bid >> 4; w.sub = w.bid & 15;
+  w.ownedTile = w.bid / kPer; w.sub = w.bid % kPer;
   return w;
 }
-// the staged radiance of sample k at lane li of block bid (stage row k, slot bid * 256 + li)
+// The staged radiance of sample k at lane li of block bid: stage row k, in the 256-thread (16 x 16 block) slot order
+// sail_accum_kernel reads -- slot (ownedTile * 16 + block16) * 256 + (y mod 16) * 16 + (x mod 16) -- whatever NT is
+template <int NT = 256>
 D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
-  A.stage[(size_t)k * (size_t)A.stageStride + (size_t)bid * 256 + li] = make_float4(e.x, e.y, e.z, 0.0f);
+  size_t slot;
+  if (NT == 256) {
+    slot = (size_t)bid * 256 + li;
+  } else {  // a 16 x NT/16 strip: sub-block column (bid mod 4), rows (bid / 4 mod kPer/4) * NT/16 + li / 16
+    constexpr int kPer = 4096 / NT;
+    const int ownedTile = bid / kPer, sub = bid % kPer;
+    const int ly = (sub >> 2) * (NT / 16) + (li >> 4), lx = (sub & 3) * 16 + (li & 15);
+    slot = ((size_t)ownedTile * 16 + (size_t)((ly >> 4) * 4 + (lx >> 4))) * 256 + (size_t)((ly & 15) * 16 + (lx & 15));
+  }
+  A.stage[(size_t)k * (size_t)A.stageStride + slot] = make_float4(e.x, e.y, e.z, 0.0f);
 }
 
 }  // namespace
@@ -1675,6 +1688,16 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
+#ifndef SAIL_SORT_ROTATE
+#define SAIL_SORT_ROTATE 0
+#endif
+#ifndef SAIL_SORT_BALLOT
+#define SAIL_SORT_BALLOT 0
+#endif
+// SAIL_KEY_RANK: the by-row key in the host's order (SailTraceArgs.keyRank, by decreasing bounds area) instead of row order
+#ifndef SAIL_KEY_RANK
+#define SAIL_KEY_RANK 0
+#endif
 // the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
 #ifndef SAIL_SCAN_DPP
 #define SAIL_SCAN_DPP 1
@@ -1699,7 +1722,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 // wider barrier.
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
-  static_assert(NT == 256 || ((NT == 128 || NT == 512 || NT == 1024) && !GROUPED), "grouped kernels share the 256-thread stage layout");
+  static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
   __shared__ float sSt[kFields][NT];
@@ -1708,10 +1731,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
-  TileWork tw = tileWork<GROUPED>(A);
-  if (NT != 256) {
-    tw.bid = (int)blockIdx.x; tw.ownedTile = tw.bid / (4096 / NT); tw.sub = tw.bid % (4096 / NT);
-  }
+  // SAIL_SORT_BALLOT (flat kernels, scenes of <= 7 rows): per-wave key counts by ballots into a (key, wave) table
+  constexpr bool ballotSort = SAIL_SORT_BALLOT && !CULL && NT == 256;
+  constexpr int kBalKeys = 8;
+  __shared__ int sWC[ballotSort ? kBalKeys * (NT / 64) : 1];
+  const TileWork tw = tileWork<GROUPED, NT>(A);
   const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
   const int sub = tw.sub;
@@ -1740,6 +1764,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (CULL) __asm__ volatile("" ::: "a0");
 #endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
+  if (ballotSort && li < kBalKeys * (NT / 64)) sWC[li] = 0;  // key 0 (dead) entries stay 0
+  const bool useBallot = ballotSort && SAIL_SORT_BY_PRIM && A.n < kBalKeys;
   int ph = 0;
   __syncthreads();
   // sort key: the winning primitive row when there are few enough rows (no row reads for the key, and a wave's
@@ -1766,7 +1792,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   auto settlePrev = [&](bool alive) {
     if (valid && kPrev >= 0) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
-      if (grouped) stageSample(A, kPrev, tw.bid, li, er);
+      if (grouped) stageSample<NT>(A, kPrev, tw.bid, li, er);
       else accumulateSample(acc, er, constRow<SailSample>(A.samples, kPrev), A.accumMode);
     }
     if (!alive) { sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f; }
@@ -1801,7 +1827,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           }
           alive = false;
         } else if (byPrim) {
+#if SAIL_KEY_RANK
+          // rows in the host's sort order (keyRank): small primitives' keys last, next to each other
+          key = 1 + (A.n <= 16 ? (int)((A.keyRank >> (4 * sw.bi)) & 15ull) : sw.bi);
+#else
           key = 1 + sw.bi;
+#endif
         } else {
           const SailPrim& p = PRIM(c, sw.bi);
           int mc = matCat(p);
@@ -1815,9 +1846,50 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
       PHASE_MARK(pc, 0);
       // ---- counting sort of the live paths by key (LDS atomics for the per-key rank, one wave scans)
+      // SAIL_SORT_ROTATE: the sorted range starts at wave (block + bounce) mod waves instead of wave 0, so the
+      // workgroup's last (most mixed) keys land on a different wave -- and SIMD -- from one block and bounce to the next
+      const int rot = SAIL_SORT_ROTATE ? (int)(((blockIdx.x + (unsigned)depth) % (unsigned)(NT / 64)) * 64u) : 0;
       int rank = 0;
       int nAlive;
-      if constexpr (twoBar) {
+      // a path's state into sorted slot d
+      auto scatterTo = [&](int d) {
+        sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
+        sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
+        sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
+        sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
+        sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
+      };
+      if (useBallot) {
+        // Keys 1..7 (row + 1; 0 = dead): each wave counts its paths per key with one ballot per key and ranks its
+        // lanes by mbcnt -- no LDS atomics -- and writes its counts into the (key, wave) table; after one barrier every
+        // wave scans the 32-entry table itself (key-major, so a key's paths are contiguous, waves in order within it).
+        // The table is rewritten only after the scatter barrier, once every wave has read it: two barriers per bounce.
+        unsigned long long my = 0ull;
+        int cntLane = 0;
+#pragma unroll
+        for (int k = 1; k < kBalKeys; k++) {
+          const unsigned long long mk = __builtin_amdgcn_ballot_w64(alive && key == k);
+          my = (key == k) ? mk : my;
+          cntLane = (lane == k) ? (int)__popcll(mk) : cntLane;
+        }
+        rank = __builtin_amdgcn_mbcnt_hi((unsigned)(my >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)my, 0u));
+        if (lane >= 1 && lane < kBalKeys) sWC[lane * (NT / 64) + wave] = cntLane;
+        __syncthreads();
+        const int v = lane < kBalKeys * (NT / 64) ? sWC[lane] : 0;
+#if SAIL_SCAN_DPP
+        const int incl = waveScanIncl(v);
+#else
+        int incl = v;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += u;
+        }
+#endif
+        nAlive = __builtin_amdgcn_readlane(incl, 63);
+        const int start = __shfl(incl - v, key * (NT / 64) + wave, 64);
+        if (alive) scatterTo((start + rank + rot) & (NT - 1));
+        __syncthreads();
+      } else if constexpr (twoBar) {
       // every wave scans the counts itself (the start of a lane's key by a cross-lane read), so no barrier
       // between the scan and the scatter; the counts alternate between two buffers, the one just read being
       // cleared by wave 0 after the scatter barrier, two bounces before it is counted into again
@@ -1838,7 +1910,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         nAlive = __builtin_amdgcn_readlane(incl, 63);
         const int start = __shfl(incl - v, key, 64);
         if (alive) {
-          const int d = start + rank;
+          const int d = (start + rank + rot) & (NT - 1);
           sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
           sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
           sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
@@ -1872,7 +1944,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       __syncthreads();
       nAlive = sStart[kKeys];
       if (alive) {
-        const int d = sStart[key] + rank;
+        const int d = (sStart[key] + rank + rot) & (NT - 1);
         sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
         sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
         sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
@@ -1881,7 +1953,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
       __syncthreads();
       }
-      alive = li < nAlive;
+      alive = ((li - rot) & (NT - 1)) < nAlive;
       PHASE_MARK(pc, 7);
       if (alive) {
         ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
@@ -1911,7 +1983,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     __syncthreads();
     if (valid) {
       const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
-      if (grouped) stageSample(A, k, tw.bid, li, er);
+      if (grouped) stageSample<NT>(A, k, tw.bid, li, er);
       else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
@@ -1942,12 +2014,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 
 // each plugin set has an ungrouped kernel (one workgroup per 16x16 block, every sample) and a _grouped one
 // (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel)
-#define SAIL_TRACE_KERNELS_NT(name, waves, body, cull, ks, km, kt, kl, nt)                                       \
+#define SAIL_TRACE_KERNELS_NT(name, waves, body, cull, ks, km, kt, kl, nt, gnt)                                  \
   extern "C" __global__ void __launch_bounds__(nt, waves) name(SailTraceArgs A) {                                \
     body<cull, false, ks, km, kt, kl, nt>(A);                                                                    \
   }                                                                                                              \
-  extern "C" __global__ void __launch_bounds__(256, waves) name##_grouped(SailTraceArgs A) {                     \
-    body<cull, true, ks, km, kt, kl>(A);                                                                         \
+  extern "C" __global__ void __launch_bounds__(gnt, waves) name##_grouped(SailTraceArgs A) {                     \
+    body<cull, true, ks, km, kt, kl, gnt>(A);                                                                    \
   }
 #define SAIL_TRACE_KERNELS(name, waves, body, cull, ks, km, kt, kl)                                              \
   extern "C" __global__ void __launch_bounds__(256, waves) name(SailTraceArgs A) {                               \
@@ -1973,7 +2045,7 @@ SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, SAIL_GENERIC_TILE, f
 #endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
                       SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS,
-                      SAIL_CORNELL_NT)
+                      SAIL_CORNELL_NT, 256)
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
 #ifndef SAIL_TRACE_ROOM_MIN_WAVES
 #define SAIL_TRACE_ROOM_MIN_WAVES 7
@@ -1988,7 +2060,7 @@ SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, S
 #define SAIL_ROOM_NT 256
 #endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
-                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT)
+                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, 256)
 // the pre-cull kernel serves scenes with many primitives (C4: 7 waves measured best of 5-8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
@@ -2000,7 +2072,12 @@ SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_RO
 #ifndef SAIL_CULL_NT
 #define SAIL_CULL_NT 1024
 #endif
-SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT)
+// threads per workgroup of the grouped pre-cull kernel (sample groups of small per-rank frames)
+#ifndef SAIL_CULL_GROUP_NT
+#define SAIL_CULL_GROUP_NT 256
+#endif
+SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT,
+                      SAIL_CULL_GROUP_NT)
 
 // ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
 extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {
@@ -2259,14 +2336,14 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
   const bool g = A.sampleGroups > 1;
 #define SAIL_LAUNCH(k) hipLaunchKernelGGL(g ? k##_grouped : k, dim3(blocks), dim3(256), 0, s, A)
   // ungrouped launches of an NT-thread kernel: blocks = ownedTiles * 16 of 256 threads -> ownedTiles * 4096 / NT
-#define SAIL_LAUNCH_NT(k, nt)                                                                   \
+#define SAIL_LAUNCH_NT(k, nt, gnt)                                                              \
   do {                                                                                          \
-    if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks), dim3(256), 0, s, A);                   \
+    if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks * 256 / (gnt)), dim3(gnt), 0, s, A);     \
     else hipLaunchKernelGGL(k, dim3(blocks * 256 / (nt)), dim3(nt), 0, s, A);                     \
   } while (0)
-  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT);
-  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT);
-  else if (A.cullPrims) SAIL_LAUNCH_NT(sail_trace_kernel_cull, SAIL_CULL_NT);
+  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT, 256);
+  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT, 256);
+  else if (A.cullPrims) SAIL_LAUNCH_NT(sail_trace_kernel_cull, SAIL_CULL_NT, SAIL_CULL_GROUP_NT);
   else SAIL_LAUNCH(sail_trace_kernel);
 #undef SAIL_LAUNCH
 #undef SAIL_LAUNCH_NT

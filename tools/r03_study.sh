@@ -8,6 +8,7 @@ mkdir -p $OUT
 P="timeout -k 10 300 python -u tools/scaling_probe.py"
 $P C4 32 > $OUT/scale_c4_auto.jsonl 2>&1 || { tail $OUT/scale_c4_auto.jsonl; exit 2; }
 for g in 1 2 4; do $P C4 32 --groups $g > $OUT/scale_c4_g$g.jsonl 2>&1 || { tail $OUT/scale_c4_g$g.jsonl; exit 3; }; done
+for g in 2 4; do $P C4 32 --groups $g --lib sail_amd/lib/variants/libsail_hip_g_cullg1024.so > $OUT/scale_c4_g${g}_nt1024.jsonl 2>&1 || { tail $OUT/scale_c4_g${g}_nt1024.jsonl; exit 3; }; done
 $P C3 256 > $OUT/scale_c3.jsonl 2>&1 || { tail $OUT/scale_c3.jsonl; exit 4; }
 $P C5 256 > $OUT/scale_c5.jsonl 2>&1 || { tail $OUT/scale_c5.jsonl; exit 5; }
 $P C2 256 > $OUT/scale_c2.jsonl 2>&1 || { tail $OUT/scale_c2.jsonl; exit 6; }

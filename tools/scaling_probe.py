@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--groups", type=int, default=0)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--lib", default=None, help="a variant build of libsail_hip.so (tools/build_variants.sh)")
     a = ap.parse_args()
+    if a.lib:
+        capi._lib = capi.load(a.lib)
     cfg = bench.CONFIGS[a.config]
     spp = a.spp
     W, H, B = cfg["width"], cfg["height"], cfg["bounces"]
@@ -61,7 +64,7 @@ def main():
             rate = work / best / 1e9
             if base is None:
                 base = rate
-            print(json.dumps({"config": a.config, "partition": "tiles" if part == capi.PART_TILES else "samples",
+            print(json.dumps({"lib": os.path.basename(a.lib) if a.lib else "main", "config": a.config, "partition": "tiles" if part == capi.PART_TILES else "samples",
                               "spp": spp, "groups": a.groups or "auto", "world": world, "rank": rank,
                               "share": round(share, 5), "s": round(best, 4), "launches": int(st.launches),
                               "Gseg_per_s_per_gpu": round(rate, 3), "vs_1gpu": round(rate / base, 3),
