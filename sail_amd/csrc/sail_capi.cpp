@@ -1,7 +1,6 @@
 // sail_capi.cpp — libsail_hip.so: context, scene decode, launches, readback, filter, RCCL reduce.
 // The C ABI is declared (with the reference interface each entry replaces) in include/sail_hip.h.
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <dlfcn.h>
 #include <math.h>
 #include <cmath>
@@ -170,7 +169,6 @@ struct sail_ctx {
   // (global sample index already counted in k), the bounce count and eye they were queued with
   std::vector<SailSample> queued;
   int queuedBounces = 0;
-  unsigned long long keyRank = 0;  // SailTraceArgs.keyRank of the current scene
   float eyeCache[3] = {0.0f, 0.0f, 0.0f};
   std::string err;
 };
@@ -439,32 +437,6 @@ void padPrimBounds(std::vector<SailPrim>& prims, const std::vector<PrimBox>& raw
   }
 }
 
-// Sort order of the compacting kernels' by-row path key (scenes of < 16 rows): rows by decreasing surface area of
-// their bounds, unbounded and unknown rows first, ties by row. The small primitives' keys come last and next to
-// each other, so the few paths that hit them share the workgroup's last wave instead of making the boundary waves
-// of large keys mixed (a wave running two shapes' hit records and materials). Only the lane a path is shaded in
-// changes: results are the same bits in any order.
-unsigned long long keyRanks(const std::vector<SailPrim>& prims) {
-  const int n = (int)prims.size();
-  if (n <= 0 || n > 16) return 0;
-  std::vector<double> area((size_t)n);
-  for (int i = 0; i < n; i++) {
-    double d[3];
-    bool finite = prims[i].type != 0;
-    for (int k = 0; k < 3; k++) {
-      d[k] = (double)prims[i].a[21 + k] - (double)prims[i].a[18 + k];
-      if (!std::isfinite(d[k])) finite = false;
-    }
-    area[i] = finite ? 2.0 * (d[0] * d[1] + d[1] * d[2] + d[0] * d[2]) : INFINITY;
-  }
-  std::vector<int> order((size_t)n);
-  for (int i = 0; i < n; i++) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return area[x] > area[y]; });
-  unsigned long long packed = 0;
-  for (int r = 0; r < n; r++) packed |= (unsigned long long)r << (4 * order[r]);
-  return packed;
-}
-
 // Largest padded-bound coordinate of the scene, inf when a primitive has no finite bound. Every ray origin
 // is the eye or a hit point inside some padded box, so |origin| <= max(extent, |eye|) (see cullFmaOk).
 double primExtent(const std::vector<SailPrim>& prims) {
@@ -630,19 +602,27 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.cullPrims = c->n >= c->cullMinPrims ? (cullFmaOk(c) ? 2 : 1) : 0;
     A.cullPrimary = eyeNearScene(c);
     A.kernelSet = kernelSetFor(c);
-    A.keyRank = c->keyRank;
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
     // = 1,016 workgroups = 4 waves per SIMD); split the launch's samples over G workgroups per block so
     // that about 4 rounds of 7-wave-per-SIMD residency are queued, and add the staged samples in order.
     int G = 1;
-    {
+    if (c->forceGroups > 0) {
+      G = c->forceGroups;
+    } else if (A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims) {
+      // The pre-cull kernel's workgroups are 1,024 threads, two per CU at 8 waves per SIMD. Its per-workgroup cost
+      // varies with the primitives a 16x64 strip sees, so a grid of few rounds ends in a long tail (1/8 of C4: 1,020
+      // workgroups = 2 rounds, 0.92 of the one-GPU rate per GPU): below 6 rounds, split the samples so that about 8
+      // rounds are queued (the grouped kernel is 1,024 threads too; measured 0.95 at N = 8 with 4 groups).
+      const double rounds = (double)owned * 4.0 / (double)(c->numCUs * 2);
+      if (rounds < 6.0) G = (int)ceil(8.0 / rounds);
+    } else {
       const long long waves = (long long)owned * 16 * 4;
       const long long target = (long long)c->numCUs * 4 * 7 * 4;
-      G = c->forceGroups > 0 ? c->forceGroups : (int)((target + waves - 1) / waves);
-      if (G > nspp) G = nspp;
-      if (G < 1) G = 1;
+      G = (int)((target + waves - 1) / waves);
     }
+    if (G > nspp) G = nspp;
+    if (G < 1) G = 1;
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
     A.stageStride = (long long)owned * 4096;
@@ -1025,7 +1005,6 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
   c->primExtent = primExtent(prims);
-  c->keyRank = keyRanks(prims);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -1069,7 +1048,6 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, c->tpRows.data(), c->tn);
   c->primExtent = primExtent(prims);
-  c->keyRank = keyRanks(prims);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -71,8 +71,6 @@ struct SailTraceArgs {
   int sampleGroups, groupSpp;
   float4* stage;
   long long stageStride;    // slots per sample = ownedTiles * 4096
-  // sort order of the by-row path key (rows < 16): 4-bit rank of row i at bits 4i..4i+3 (sail_capi.cpp keyRanks)
-  unsigned long long keyRank;
 };
 
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a

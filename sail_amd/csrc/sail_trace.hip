@@ -1688,15 +1688,9 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
-#ifndef SAIL_SORT_ROTATE
-#define SAIL_SORT_ROTATE 0
-#endif
-#ifndef SAIL_SORT_BALLOT
-#define SAIL_SORT_BALLOT 0
-#endif
-// SAIL_KEY_RANK: the by-row key in the host's order (SailTraceArgs.keyRank, by decreasing bounds area) instead of row order
-#ifndef SAIL_KEY_RANK
-#define SAIL_KEY_RANK 0
+// SAIL_PRIO_MIXED = p: after the sort, a wave whose paths won different rows runs at issue priority p (study switch)
+#ifndef SAIL_PRIO_MIXED
+#define SAIL_PRIO_MIXED 0
 #endif
 // the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
 #ifndef SAIL_SCAN_DPP
@@ -1731,10 +1725,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
-  // SAIL_SORT_BALLOT (flat kernels, scenes of <= 7 rows): per-wave key counts by ballots into a (key, wave) table
-  constexpr bool ballotSort = SAIL_SORT_BALLOT && !CULL && NT == 256;
-  constexpr int kBalKeys = 8;
-  __shared__ int sWC[ballotSort ? kBalKeys * (NT / 64) : 1];
   const TileWork tw = tileWork<GROUPED, NT>(A);
   const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
@@ -1764,8 +1754,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (CULL) __asm__ volatile("" ::: "a0");
 #endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
-  if (ballotSort && li < kBalKeys * (NT / 64)) sWC[li] = 0;  // key 0 (dead) entries stay 0
-  const bool useBallot = ballotSort && SAIL_SORT_BY_PRIM && A.n < kBalKeys;
   int ph = 0;
   __syncthreads();
   // sort key: the winning primitive row when there are few enough rows (no row reads for the key, and a wave's
@@ -1827,12 +1815,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           }
           alive = false;
         } else if (byPrim) {
-#if SAIL_KEY_RANK
-          // rows in the host's sort order (keyRank): small primitives' keys last, next to each other
-          key = 1 + (A.n <= 16 ? (int)((A.keyRank >> (4 * sw.bi)) & 15ull) : sw.bi);
-#else
           key = 1 + sw.bi;
-#endif
         } else {
           const SailPrim& p = PRIM(c, sw.bi);
           int mc = matCat(p);
@@ -1846,9 +1829,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
       PHASE_MARK(pc, 0);
       // ---- counting sort of the live paths by key (LDS atomics for the per-key rank, one wave scans)
-      // SAIL_SORT_ROTATE: the sorted range starts at wave (block + bounce) mod waves instead of wave 0, so the
-      // workgroup's last (most mixed) keys land on a different wave -- and SIMD -- from one block and bounce to the next
-      const int rot = SAIL_SORT_ROTATE ? (int)(((blockIdx.x + (unsigned)depth) % (unsigned)(NT / 64)) * 64u) : 0;
       int rank = 0;
       int nAlive;
       // a path's state into sorted slot d
@@ -1859,37 +1839,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
         sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
       };
-      if (useBallot) {
-        // Keys 1..7 (row + 1; 0 = dead): each wave counts its paths per key with one ballot per key and ranks its
-        // lanes by mbcnt -- no LDS atomics -- and writes its counts into the (key, wave) table; after one barrier every
-        // wave scans the 32-entry table itself (key-major, so a key's paths are contiguous, waves in order within it).
-        // The table is rewritten only after the scatter barrier, once every wave has read it: two barriers per bounce.
-        unsigned long long my = 0ull;
-        int cntLane = 0;
-#pragma unroll
-        for (int k = 1; k < kBalKeys; k++) {
-          const unsigned long long mk = __builtin_amdgcn_ballot_w64(alive && key == k);
-          my = (key == k) ? mk : my;
-          cntLane = (lane == k) ? (int)__popcll(mk) : cntLane;
-        }
-        rank = __builtin_amdgcn_mbcnt_hi((unsigned)(my >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)my, 0u));
-        if (lane >= 1 && lane < kBalKeys) sWC[lane * (NT / 64) + wave] = cntLane;
-        __syncthreads();
-        const int v = lane < kBalKeys * (NT / 64) ? sWC[lane] : 0;
-#if SAIL_SCAN_DPP
-        const int incl = waveScanIncl(v);
-#else
-        int incl = v;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int u = __shfl_up(incl, off, 64);
-          if (lane >= off) incl += u;
-        }
-#endif
-        nAlive = __builtin_amdgcn_readlane(incl, 63);
-        const int start = __shfl(incl - v, key * (NT / 64) + wave, 64);
-        if (alive) scatterTo((start + rank + rot) & (NT - 1));
-        __syncthreads();
-      } else if constexpr (twoBar) {
+      if constexpr (twoBar) {
       // every wave scans the counts itself (the start of a lane's key by a cross-lane read), so no barrier
       // between the scan and the scatter; the counts alternate between two buffers, the one just read being
       // cleared by wave 0 after the scatter barrier, two bounces before it is counted into again
@@ -1909,14 +1859,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #endif
         nAlive = __builtin_amdgcn_readlane(incl, 63);
         const int start = __shfl(incl - v, key, 64);
-        if (alive) {
-          const int d = (start + rank + rot) & (NT - 1);
-          sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
-          sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
-          sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
-          sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
-          sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
-        }
+        if (alive) scatterTo(start + rank);
       }
       __syncthreads();
       if (wave == 0) sCnt2[ph][lane] = 0;
@@ -1943,17 +1886,19 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
       __syncthreads();
       nAlive = sStart[kKeys];
-      if (alive) {
-        const int d = (sStart[key] + rank + rot) & (NT - 1);
-        sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
-        sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
-        sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
-        sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
-        sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
-      }
+      if (alive) scatterTo(sStart[key] + rank);
       __syncthreads();
       }
-      alive = ((li - rot) & (NT - 1)) < nAlive;
+      alive = li < nAlive;
+#if SAIL_PRIO_MIXED
+      {  // a wave holding paths of several keys runs several hit-record / material branches: raise its issue priority
+        // so that its workgroup's next barrier is not held up by it (the others wait there)
+        const int b0 = __builtin_amdgcn_readfirstlane(__float_as_int(sSt[10][li]));
+        const bool mixed = __builtin_amdgcn_ballot_w64(alive && __float_as_int(sSt[10][li]) != b0) != 0ull;
+        if (mixed) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#endif
       PHASE_MARK(pc, 7);
       if (alive) {
         ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
@@ -2074,7 +2019,7 @@ SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_RO
 #endif
 // threads per workgroup of the grouped pre-cull kernel (sample groups of small per-rank frames)
 #ifndef SAIL_CULL_GROUP_NT
-#define SAIL_CULL_GROUP_NT 256
+#define SAIL_CULL_GROUP_NT 1024
 #endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT,
                       SAIL_CULL_GROUP_NT)

@@ -359,6 +359,35 @@ def test_kernel_selection(gpu, fixtures):
 
 
 # ---- sample groups (small per-rank frames): staged samples added in order are bit-identical ---------------------
+@pytest.mark.parametrize("groups", [0, 3, 4])
+@pytest.mark.parametrize("rank,world", [(0, 1), (1, 3)])
+def test_precull_sample_groups_multi_tile(gpu, fixtures, groups, rank, world):
+    """the pre-cull kernel's grouped form (1,024-thread workgroups, 16x64 strips) stages each sample in the 16x16
+    slot order sail_accum_kernel reads: several tiles, ragged edges, a tile rank, the host's own group rule (0)"""
+    sc = fixtures["scenes"]["C4"]
+    W, H, B, spp = 150, 140, 4, 6
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    ctx = capi.Context(W, H, flags=capi.FLAG_AOV)
+    try:
+        if groups:
+            ctx.set_debug(capi.DEBUG_SAMPLE_GROUPS, groups)
+        ctx.set_scene_dict(sc)
+        assert ctx.kernel_name() == "sail_trace_kernel_cull"
+        ctx.set_partition(rank, world)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got, gn, gp = ctx.readback(aov=True)
+        acc = ctx.read_accum()
+    finally:
+        ctx.close()
+    want, wn, wp = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B, aov=True)
+    tx = (W + 63) // 64
+    yy, xx = np.mgrid[0:H, 0:W]
+    mine = (((yy // 64) * tx + xx // 64) % world) == rank
+    assert bit_equal(acc[mine], want[mine]).all()
+    assert (acc[~mine] == 0).all()
+    assert bit_equal(gn[mine], wn[mine]).all() and bit_equal(gp[mine], wp[mine]).all()
+
+
 @pytest.mark.parametrize("name", ["C1", "C3", "C4"])   # C4: the pre-cull kernel, 1024 threads when ungrouped
 @pytest.mark.parametrize("groups", ["1", "2", "5"])
 @pytest.mark.parametrize("mode", [capi.ACCUM_SUM, capi.ACCUM_MIX])
