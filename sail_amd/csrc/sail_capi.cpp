@@ -1,6 +1,7 @@
 // sail_capi.cpp — libsail_hip.so: context, scene decode, launches, readback, filter, RCCL reduce.
 // The C ABI is declared (with the reference interface each entry replaces) in include/sail_hip.h.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <dlfcn.h>
 #include <math.h>
 #include <cmath>
@@ -169,6 +170,7 @@ struct sail_ctx {
   // (global sample index already counted in k), the bounce count and eye they were queued with
   std::vector<SailSample> queued;
   int queuedBounces = 0;
+  unsigned char keyOfRow[64] = {0}, segOfKey[64] = {0};  // task layout tables (shadeClasses)
   float eyeCache[3] = {0.0f, 0.0f, 0.0f};
   std::string err;
 };
@@ -437,6 +439,34 @@ void padPrimBounds(std::vector<SailPrim>& prims, const std::vector<PrimBox>& raw
   }
 }
 
+// Task layout of the sorted paths (traceTileTasks; scenes of < 64 rows): a row's shading class is its material
+// category and whether it emits (an emitting matte surface takes no light sample). Rows ordered by (class, row) get
+// the sort keys 1, 2, ...; each class's first key starts a new 64-lane task, so a task shades one class. Key 0 (a
+// path that left the scene) and the unused keys past the last row form classes of their own, always empty.
+void shadeClasses(const std::vector<SailPrim>& prims, unsigned char keyOfRow[64], unsigned char segOfKey[64]) {
+  const int n = (int)prims.size();
+  memset(keyOfRow, 0, 64);
+  memset(segOfKey, 0, 64);
+  if (n <= 0 || n >= 64) return;
+  std::vector<int> cls((size_t)n), order((size_t)n);
+  for (int i = 0; i < n; i++) {
+    int mc = (int)(short)(prims[i].cats & 0xffff);
+    mc = (mc >= 0 && mc < 5) ? mc : 0;
+    const bool emits = prims[i].em[0] != 0.0f || prims[i].em[1] != 0.0f || prims[i].em[2] != 0.0f;
+    cls[i] = mc * 2 + (emits ? 1 : 0);
+    order[i] = i;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cls[a] < cls[b]; });
+  int seg = 0, prev = -1;
+  for (int r = 0; r < n; r++) {
+    const int row = order[r];
+    if (cls[row] != prev) { seg++; prev = cls[row]; }
+    keyOfRow[row] = (unsigned char)(1 + r);
+    segOfKey[1 + r] = (unsigned char)seg;
+  }
+  for (int key = n + 1; key < 64; key++) segOfKey[key] = (unsigned char)(seg + 1);
+}
+
 // Largest padded-bound coordinate of the scene, inf when a primitive has no finite bound. Every ray origin
 // is the eye or a hit point inside some padded box, so |origin| <= max(extent, |eye|) (see cullFmaOk).
 double primExtent(const std::vector<SailPrim>& prims) {
@@ -602,6 +632,8 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.cullPrims = c->n >= c->cullMinPrims ? (cullFmaOk(c) ? 2 : 1) : 0;
     A.cullPrimary = eyeNearScene(c);
     A.kernelSet = kernelSetFor(c);
+    memcpy(A.keyOfRow, c->keyOfRow, sizeof A.keyOfRow);
+    memcpy(A.segOfKey, c->segOfKey, sizeof A.segOfKey);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
     // = 1,016 workgroups = 4 waves per SIMD); split the launch's samples over G workgroups per block so
@@ -1005,6 +1037,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
   c->primExtent = primExtent(prims);
+  shadeClasses(prims, c->keyOfRow, c->segOfKey);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -1048,6 +1081,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, c->tpRows.data(), c->tn);
   c->primExtent = primExtent(prims);
+  shadeClasses(prims, c->keyOfRow, c->segOfKey);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));

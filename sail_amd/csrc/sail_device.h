@@ -71,6 +71,10 @@ struct SailTraceArgs {
   int sampleGroups, groupSpp;
   float4* stage;
   long long stageStride;    // slots per sample = ownedTiles * 4096
+  // task layout of the sorted paths (traceTileTasks, scenes of < 64 rows): each row's sort key (1 + its position in
+  // the rows ordered by shading class) and each key's class; a class starts a new wave (sail_capi.cpp shadeClasses)
+  unsigned char keyOfRow[64];
+  unsigned char segOfKey[64];
 };
 
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a

@@ -1948,6 +1948,206 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
   }
 }
+// ---- task layout of the sorted paths (SAIL_ROOM_TILE=traceTileTasks) -------------------------------------------------
+// traceTileCompact packs the sorted paths contiguously, so the few paths of each small key share the workgroup's last
+// wave: in the C3 room that wave runs the metal, mirror, glass and lit-matte branches one after another while the
+// other waves wait at the next barrier. Here the sorted order is laid out in 64-slot "tasks": each shading class (the
+// rows' material, and whether they emit, sail_capi.cpp shadeClasses) starts a new task, so a task holds paths of one
+// class, and the waves take the tasks round robin (up to kMaxTasks: several per wave). Each path keeps a home slot
+// (its pixel's lane): the home lane sweeps the path's ray (dense, every lane of a wave busy) and counts its key; the
+// sorted order is a permutation of home slots, and the task lanes read the path's state from its home slot, shade it
+// and write the next ray back home. Three barriers per bounce; no end-of-sample barriers (a pixel's radiance slot is
+// its home lane's). Only the lane that shades a path changes: the result is bit-identical.
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
+__device__ __forceinline__ void traceTileTasks(const SailTraceArgs& A) {
+  static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
+  constexpr int NW = NT / 64;
+  constexpr int kKeys = 64;
+  constexpr int kMaxTasks = 3 * NW;        // room for every class to start its own task, up to 3 rounds
+  // home state: ray o, d (0..5), throughput (6..8), winning row (9), distance (10), local hit point (11..13)
+  __shared__ float sSt[14][NT];
+  __shared__ float sE[3][NT];
+  __shared__ int sCnt[kKeys];
+  __shared__ short sPerm[kMaxTasks * 64];
+  const TileWork tw = tileWork<GROUPED, NT>(A);
+  const int ownedTile = tw.ownedTile;
+  if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
+  const int sub = tw.sub;
+  const int tile = A.rank + ownedTile * A.world;
+  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
+  const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
+  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * (NT / 16);
+  const int x = x0 + (li & 15), y = y0 + (li >> 4);
+  const bool valid = x < A.W && y < A.H;
+
+  Ctx c;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
+  c.prims = A.prims;
+  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
+  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
+  c.fcx = 0.0f; c.fcy = 0.0f;
+  c.shadowAnyHit = A.shadowAnyHit;
+  c.cullPrims = CULL ? 1 : 0;
+  c.cullFma = CULL && A.cullPrims == 2;
+  c.cullPrimary = A.cullPrimary;
+  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
+
+  if (li < kKeys) sCnt[li] = 0;
+  // rows -> keys in shading-class order (host tables) when the scene has few rows, else (material, shape)
+  const bool byPrim = A.n < kKeys;
+  // this lane's key (= lane) and its class; a class's first key starts a task
+  const int segL = byPrim ? (int)A.segOfKey[lane] : (lane + 9) / 10;
+  const int segNext = lane == 63 ? -1 : (byPrim ? (int)A.segOfKey[lane + 1] : (lane + 10) / 10);
+  const bool firstOfSeg = lane == 0 || segL != (byPrim ? (int)A.segOfKey[lane - 1] : (lane + 8) / 10);
+  const bool lastOfSeg = segNext != segL;
+  __syncthreads();
+  const size_t pixG = (size_t)y * A.W + x;
+  constexpr bool grouped = GROUPED;
+  float4 acc = (valid && !grouped) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
+  const bool tri0 = s + t <= 1.0f;
+  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
+  unsigned segs = 0;
+  PhaseClock pc;
+#if SAIL_PHASE_TIMING
+  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
+  pc.t = __builtin_amdgcn_s_memtime();
+#endif
+  for (int k = tw.kBeg; k < tw.kEnd; k++) {
+    const SailSample& S = constRow<SailSample>(A.samples, k);
+    const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
+    bool alive = valid;
+    // the path's radiance lives in LDS at its pixel (its home lane), updated in bounce order
+    sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f;
+    for (int depth = 1; depth <= A.maxBounces; depth++) {
+      // ---- phase A (home lane): the path's sweep and its key
+      int key = 0;
+      if (alive) {
+        Ray ray;
+        if (depth == 1) {
+          const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
+          const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
+          ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
+          sSt[0][li] = ray.o.x; sSt[1][li] = ray.o.y; sSt[2][li] = ray.o.z;
+          sSt[3][li] = ray.d.x; sSt[4][li] = ray.d.y; sSt[5][li] = ray.d.z;
+          sSt[6][li] = 1.0f; sSt[7][li] = 1.0f; sSt[8][li] = 1.0f;
+        } else {
+          ray = mkRay(v3(sSt[0][li], sSt[1][li], sSt[2][li]), v3(sSt[3][li], sSt[4][li], sSt[5][li]));
+        }
+        segs++;
+        const Sweep sw = sweepRay(c, ray, depth == 1);
+        if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
+          if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
+            const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
+            if (A.aovN) A.aovN[pixG] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+            if (A.aovP) A.aovP[pixG] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+          }
+          alive = false;
+        } else {
+          if (byPrim) {
+            key = (int)A.keyOfRow[sw.bi];
+          } else {
+            const SailPrim& p = PRIM(c, sw.bi);
+            int mc = matCat(p);
+            mc = (mc >= 0 && mc < 5) ? mc : 0;
+            key = 1 + mc * 10 + p.type;
+          }
+          sSt[9][li] = __int_as_float(sw.bi); sSt[10][li] = sw.best;
+          sSt[11][li] = sw.bhl.x; sSt[12][li] = sw.bhl.y; sSt[13][li] = sw.bhl.z;
+        }
+      }
+      PHASE_MARK(pc, 0);
+      const int rank = alive ? atomicAdd(&sCnt[key], 1) : 0;
+      __syncthreads();  // B1: counts complete, home state written
+      // ---- every wave lays out the sorted order itself: key starts, each class padded to start a new task
+      int nTasks, nAlive;
+      bool padded;
+      int classEnd, classInfo;  // at a class's last key: its padded end, and (path count | padded size << 16)
+      {
+        const int v = sCnt[lane];
+        const int incl = waveScanIncl(v);
+        const int excl = incl - v;
+        nAlive = __builtin_amdgcn_readlane(incl, 63);
+        const int base = waveScanMaxIncl(firstOfSeg ? excl : 0);  // unpadded start of this key's class
+        const int total = incl - base;                              // at the class's last key: the class size
+        const int R = lastOfSeg ? ((total + 63) & ~63) : 0;
+        const int Rincl = waveScanIncl(R);
+        const int paddedTotal = __builtin_amdgcn_readlane(Rincl, 63);
+        padded = paddedTotal <= kMaxTasks * 64;
+        nTasks = padded ? paddedTotal >> 6 : (nAlive + 63) >> 6;
+        const int keyStart = padded ? (Rincl - R) + (excl - base) : excl;
+        classEnd = lastOfSeg ? Rincl : 0x7fffffff;
+        classInfo = lastOfSeg ? (total | (R << 16)) : 0;
+        const int start = __shfl(keyStart, key, 64);
+        if (alive) sPerm[start + rank] = (short)li;
+      }
+      __syncthreads();  // B2: the permutation is complete; counts read by every wave
+      if (wave == 0) sCnt[lane] = 0;
+      PHASE_MARK(pc, 7);
+      // ---- phase B (task lanes): hit record and shading of the path in each of this wave's task slots
+      for (int tk = wave; tk < nTasks; tk += NW) {
+        const int slot = tk * 64 + lane;
+        bool on;
+        if (padded) {
+          // the class holding this task: the first class (last-key lane) whose padded end lies beyond the task start
+          const unsigned long long m = __builtin_amdgcn_ballot_w64(classEnd > tk * 64);
+          const int L = (int)__builtin_ctzll(m);
+          const int endL = __builtin_amdgcn_readlane(classEnd, L);
+          const int info = __builtin_amdgcn_readlane(classInfo, L);
+          on = slot - (endL - (info >> 16)) < (info & 0xffff);
+        } else {
+          on = slot < nAlive;
+        }
+        if (!on) continue;
+        const int p = (int)sPerm[slot];
+        Ray ray;
+        ray.o = v3(sSt[0][p], sSt[1][p], sSt[2][p]);
+        ray.d = v3(sSt[3][p], sSt[4][p], sSt[5][p]);
+        ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
+        V3 fpdf = v3(sSt[6][p], sSt[7][p], sSt[8][p]);
+        Sweep sw;
+        sw.bi = __float_as_int(sSt[9][p]); sw.best = sSt[10][p];
+        sw.bhl = v3(sSt[11][p], sSt[12][p], sSt[13][p]);
+        c.fcx = (float)(x0 + (p & 15)) + 0.5f;
+        c.fcy = (float)(y0 + (p >> 4)) + 0.5f;
+        const Hit ins = hitRecordU(c, ray, sw);
+        PHASE_MARK(pc, 1);
+        if (depth == 1 && aovSample) {
+          const size_t g = (size_t)(y0 + (p >> 4)) * A.W + x0 + (p & 15);
+          const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
+          if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+          if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+        }
+        V3 e = v3(sE[0][p], sE[1][p], sE[2][p]);
+        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
+          shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+        sE[0][p] = e.x; sE[1][p] = e.y; sE[2][p] = e.z;
+        if (depth < A.maxBounces) {
+          sSt[0][p] = ray.o.x; sSt[1][p] = ray.o.y; sSt[2][p] = ray.o.z;
+          sSt[3][p] = ray.d.x; sSt[4][p] = ray.d.y; sSt[5][p] = ray.d.z;
+          sSt[6][p] = fpdf.x; sSt[7][p] = fpdf.y; sSt[8][p] = fpdf.z;
+        }
+      }
+      __syncthreads();  // B3: next rays and radiance written
+    }
+    if (valid) {
+      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
+      if (grouped) stageSample<NT>(A, k, tw.bid, li, er);
+      else accumulateSample(acc, er, S, A.accumMode);
+    }
+  }
+  if (valid && !grouped) A.accum[pixG] = acc;
+#if SAIL_PHASE_TIMING
+  if (lane == 0)
+    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
+#endif
+  if (A.segCounter) {
+    unsigned long long v = segs;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * (unsigned)NW + (unsigned)wave) % SAIL_SEG_SLOTS], v);
+  }
+}
+
 // Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;
 // earlier builds with more live state lost to spills in the flat kernels). SAIL_COMPACT=0 / SAIL_*_TILE select
 // the unsorted body for comparisons.
