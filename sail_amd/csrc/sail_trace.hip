@@ -995,28 +995,44 @@ D Sweep sweepRay(const Ctx& c, const Ray& r, bool primary) {
   Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
   return sw;
 }
+// The winner's local hit point from the ray and its distance: every local-space intersect above ends with
+// hit = o + t * d on the same local o and d (W2L of the ray for the quadrics and the disk, the rectangle's frame), so
+// this is the sweep's own value bit for bit -- the compacting kernels recompute it instead of moving it through LDS
+// (SAIL_STATE_PACK).
+D V3 quadLocalHit(const SailPrim& p, const Ray& r, float t) {
+  const V3 d = W2L(r.d), o = W2L(r.o - P3(p, 0));
+  return o + t * d;
+}
+D V3 rectLocalHit(const SailPrim& p, const Ray& r, float t) {
+  const RectFrame f = rectFrame(p);
+  const V3 d = worldToLocal(r.d, f.normal, f.ss, f.ts);
+  const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
+  return o + t * d;
+}
+template <bool RECOMP_HL = false>
 D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const float best = sw.best;
   const int bi = sw.bi;
-  const V3 bhl = sw.bhl;
   Hit h;
   h.d = best;
   // precondition: bi >= 0 is a sweep winner, so its shape is compiled into this kernel (primT returns
   // MAX_DISTANCE for any other row, which never wins): no zero record is needed on any path -- a divergent
   // zero default would be materialised for every lane before the dispatch
   const SailPrim& p = PRIM(c, bi);
+#define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
   switch (p.type) {
     case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
-    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) { rectHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) { cylinderHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, bhl, h); break; } __builtin_unreachable();
-    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, bhl, h); break; } __builtin_unreachable();
+    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) { rectHit(c, p, RECOMP_HL ? rectLocalHit(p, r, best) : sw.bhl, h); break; } __builtin_unreachable();
+    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) { cylinderHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) { cornellHit(p, r, best, h); break; } __builtin_unreachable();
     default: __builtin_unreachable();
   }
+#undef BHL
   h.matRow = p.matRow;
   h.emission = v3(p.em[0], p.em[1], p.em[2]);
   // faceObj test (shader.shape.js:47-49) on sgn(rev) * normal: (-n).d is exactly -(n.d) (negated products,
@@ -1035,16 +1051,17 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   return h;
 }
 // wave-uniform winner: the same record with the row index in an SGPR (scalar row loads)
+template <bool RECOMP_HL = false>
 D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
 #if SAIL_HIT_UNIFORM
   const int b0 = __builtin_amdgcn_readfirstlane(sw.bi);
   if (__all(sw.bi == b0)) {
     Sweep su = sw;
     su.bi = b0;
-    return hitRecord(c, r, su);
+    return hitRecord<RECOMP_HL>(c, r, su);
   }
 #endif
-  return hitRecord(c, r, sw);
+  return hitRecord<RECOMP_HL>(c, r, sw);
 }
 D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc) {
   const Sweep sw = sweepRay(c, r, primary);
@@ -1692,6 +1709,10 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_PRIO_MIXED
 #define SAIL_PRIO_MIXED 0
 #endif
+// SAIL_STATE_PACK: the migrated path state as six float2 (ds_*_b64) with the local hit point recomputed (study switch)
+#ifndef SAIL_STATE_PACK
+#define SAIL_STATE_PACK 0
+#endif
 // the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
 #ifndef SAIL_SCAN_DPP
 #define SAIL_SCAN_DPP 1
@@ -1719,7 +1740,14 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
+#if SAIL_STATE_PACK
+  // packed path state: six float2 per path, ray o / d, throughput, distance, pixel | row << 10 (ds_write_b64 /
+  // ds_read_b64: 6 + 6 LDS instructions instead of 15 + 15); the local hit point is recomputed (hitRecord<true>)
+  __shared__ float2 sSt2[6][NT];
+  (void)kFields;
+#else
   __shared__ float sSt[kFields][NT];
+#endif
   __shared__ float sE[3][NT];
   constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
@@ -1833,11 +1861,17 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int nAlive;
       // a path's state into sorted slot d
       auto scatterTo = [&](int d) {
+#if SAIL_STATE_PACK
+        sSt2[0][d] = make_float2(ray.o.x, ray.o.y); sSt2[1][d] = make_float2(ray.o.z, ray.d.x);
+        sSt2[2][d] = make_float2(ray.d.y, ray.d.z); sSt2[3][d] = make_float2(fpdf.x, fpdf.y);
+        sSt2[4][d] = make_float2(fpdf.z, sw.best); sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), 0.0f);
+#else
         sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
         sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
         sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
         sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
         sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
+#endif
       };
       if constexpr (twoBar) {
       // every wave scans the counts itself (the start of a lane's key by a cross-lane read), so no barrier
@@ -1890,17 +1924,22 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       __syncthreads();
       }
       alive = li < nAlive;
-#if SAIL_PRIO_MIXED
-      {  // a wave holding paths of several keys runs several hit-record / material branches: raise its issue priority
-        // so that its workgroup's next barrier is not held up by it (the others wait there)
-        const int b0 = __builtin_amdgcn_readfirstlane(__float_as_int(sSt[10][li]));
-        const bool mixed = __builtin_amdgcn_ballot_w64(alive && __float_as_int(sSt[10][li]) != b0) != 0ull;
-        if (mixed) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-#endif
       PHASE_MARK(pc, 7);
       if (alive) {
+#if SAIL_STATE_PACK
+        {
+          const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
+          const int pk = __float_as_int(sSt2[5][li].x);
+          ray.o = v3(q0.x, q0.y, q1.x);
+          ray.d = v3(q1.y, q2.x, q2.y);
+          fpdf = v3(q3.x, q3.y, q4.x);
+          sw.best = q4.y;
+          pixel = pk & 1023;
+          sw.bi = pk >> 10;
+          sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
+        }
+        ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
+#else
         ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
         ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
         ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
@@ -1908,9 +1947,18 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         pixel = __float_as_int(sSt[9][li]);
         sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
         sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
+#endif
+#if SAIL_PRIO_MIXED
+        {  // a wave whose live paths won different rows runs several hit-record / material branches: raise its issue
+           // priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
+          const int b0 = __builtin_amdgcn_readfirstlane(sw.bi);
+          if (__builtin_amdgcn_ballot_w64(sw.bi != b0) != 0ull) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
-        const Hit ins = hitRecordU(c, ray, sw);
+        const Hit ins = hitRecordU<SAIL_STATE_PACK != 0>(c, ray, sw);
         PHASE_MARK(pc, 1);
         if (depth == 1 && aovSample) {
           const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
@@ -2076,7 +2124,7 @@ __device__ __forceinline__ void traceTileTasks(const SailTraceArgs& A) {
         padded = paddedTotal <= kMaxTasks * 64;
         nTasks = padded ? paddedTotal >> 6 : (nAlive + 63) >> 6;
         const int keyStart = padded ? (Rincl - R) + (excl - base) : excl;
-        classEnd = lastOfSeg ? Rincl : 0x7fffffff;
+        classEnd = lastOfSeg ? Rincl : -1;  // only a class's last key is a candidate of the per-task search
         classInfo = lastOfSeg ? (total | (R << 16)) : 0;
         const int start = __shfl(keyStart, key, 64);
         if (alive) sPerm[start + rank] = (short)li;
@@ -2099,7 +2147,7 @@ __device__ __forceinline__ void traceTileTasks(const SailTraceArgs& A) {
           on = slot < nAlive;
         }
         if (!on) continue;
-        const int p = (int)sPerm[slot];
+        const int p = (int)sPerm[slot] & (NT - 1);  // a home slot (the mask keeps every access in bounds regardless)
         Ray ray;
         ray.o = v3(sSt[0][p], sSt[1][p], sSt[2][p]);
         ray.d = v3(sSt[3][p], sSt[4][p], sSt[5][p]);
@@ -2112,7 +2160,7 @@ __device__ __forceinline__ void traceTileTasks(const SailTraceArgs& A) {
         c.fcy = (float)(y0 + (p >> 4)) + 0.5f;
         const Hit ins = hitRecordU(c, ray, sw);
         PHASE_MARK(pc, 1);
-        if (depth == 1 && aovSample) {
+        if (depth == 1 && aovSample && x0 + (p & 15) < A.W && y0 + (p >> 4) < A.H) {
           const size_t g = (size_t)(y0 + (p >> 4)) * A.W + x0 + (p & 15);
           const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
