@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--no-c1-full", action="store_true", help="skip the ~30 s full C1 render of the CPU baseline")
     ap.add_argument("--force-rccl", action="store_true",
                     help="one process: the multi-device context's RCCL reduce even at --gpus 1 (SAIL_DEBUG_FORCE_RCCL)")
+    ap.add_argument("--wavefront", action="store_true",
+                    help="study: the pre-cull path by the wavefront split instead of the megakernel (SAIL_DEBUG_WAVEFRONT)")
     ap.add_argument("--no-validate", action="store_true",
                     help="skip the check of the reduced frame after the timed steps (counts + oracle crops)")
     ap.add_argument("--force-comm", action="store_true",
@@ -290,6 +292,8 @@ def main():
     ctx = capi.Context(W, H, devices=list(range(args.gpus))) if multi else capi.Context(W, H, device=local_rank)
     if multi and args.force_rccl:
         ctx.set_debug(capi.DEBUG_FORCE_RCCL, 1)
+    if args.wavefront:
+        ctx.set_debug(capi.DEBUG_WAVEFRONT, 1)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
     part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
@@ -375,7 +379,7 @@ def main():
             "dtype": "f32",
             "data": f"synthetic: frozen {cfg['desc']} scene rows (SURVEY §8(d), JS API == reference serializer), "
                     "deterministic sample schedule",
-            "config": {"workload": cfg["workload"], "width": W, "height": H, "bounces": B, "spp": spp,
+            "config": {"workload": cfg["workload"] + ("_wavefront_split" if args.wavefront else ""), "width": W, "height": H, "bounces": B, "spp": spp,
                        "launch_spp": args.launch_spp, "partition": f"tiles64x{ngpu}",
                        "processes": "one per GPU" if world > 1 else ("one (multi-device context)" if multi else "one"), "segments_per_step": W * H * spp * B},
             "roofline": {

@@ -109,7 +109,10 @@ enum sail_debug_option {
   /* multi-device contexts of distinct devices only: 1 builds the ncclCommInitAll communicator now even for ONE
    * device, so the grouped RCCL reduce (the path of N distinct GPUs) runs on a one-GPU machine [0: a one-device
    * context needs no reduce]. Refused (SAIL_E_INVALID) on a context whose devices are all the same GPU. */
-  SAIL_DEBUG_FORCE_RCCL = 5
+  SAIL_DEBUG_FORCE_RCCL = 5,
+  /* 1: scenes on the pre-cull path are traced by the wavefront split (one sample at a time, path state in HBM, sweep /
+   * shade / shadow kernels per bounce) instead of the megakernel; same results [0] */
+  SAIL_DEBUG_WAVEFRONT = 6
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 

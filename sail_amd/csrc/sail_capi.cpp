@@ -1,7 +1,6 @@
 // sail_capi.cpp — libsail_hip.so: context, scene decode, launches, readback, filter, RCCL reduce.
 // The C ABI is declared (with the reference interface each entry replaces) in include/sail_hip.h.
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <dlfcn.h>
 #include <math.h>
 #include <cmath>
@@ -21,6 +20,7 @@ hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
 hipError_t sail_launch_sum(const SailSumArgs& A, hipStream_t s);
 hipError_t sail_launch_negzero_unowned(float4* a, float4* b, int W, int H, int rank, int world, hipStream_t s);
+hipError_t sail_launch_wavefront(const SailTraceArgs& A, const SailWfState& S, hipStream_t s);
 hipError_t sail_launch_pick(const SailPrim* prims, int n, const float* rays, int count, int32_t* index, float* t,
                             hipStream_t s);
 
@@ -136,6 +136,9 @@ struct sail_ctx {
   SceneBox scene{};              // union of the primitives' finite bounds (padPrimBounds)
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
+  int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
+  float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
+  size_t wfSlots = 0;
   int numCUs = 256;
   float4* stage = nullptr;  // sample-group staging, allocated on first use
   size_t stageBytes = 0;
@@ -170,7 +173,6 @@ struct sail_ctx {
   // (global sample index already counted in k), the bounce count and eye they were queued with
   std::vector<SailSample> queued;
   int queuedBounces = 0;
-  unsigned char keyOfRow[64] = {0}, segOfKey[64] = {0};  // task layout tables (shadeClasses)
   float eyeCache[3] = {0.0f, 0.0f, 0.0f};
   std::string err;
 };
@@ -439,34 +441,6 @@ void padPrimBounds(std::vector<SailPrim>& prims, const std::vector<PrimBox>& raw
   }
 }
 
-// Task layout of the sorted paths (traceTileTasks; scenes of < 64 rows): a row's shading class is its material
-// category and whether it emits (an emitting matte surface takes no light sample). Rows ordered by (class, row) get
-// the sort keys 1, 2, ...; each class's first key starts a new 64-lane task, so a task shades one class. Key 0 (a
-// path that left the scene) and the unused keys past the last row form classes of their own, always empty.
-void shadeClasses(const std::vector<SailPrim>& prims, unsigned char keyOfRow[64], unsigned char segOfKey[64]) {
-  const int n = (int)prims.size();
-  memset(keyOfRow, 0, 64);
-  memset(segOfKey, 0, 64);
-  if (n <= 0 || n >= 64) return;
-  std::vector<int> cls((size_t)n), order((size_t)n);
-  for (int i = 0; i < n; i++) {
-    int mc = (int)(short)(prims[i].cats & 0xffff);
-    mc = (mc >= 0 && mc < 5) ? mc : 0;
-    const bool emits = prims[i].em[0] != 0.0f || prims[i].em[1] != 0.0f || prims[i].em[2] != 0.0f;
-    cls[i] = mc * 2 + (emits ? 1 : 0);
-    order[i] = i;
-  }
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cls[a] < cls[b]; });
-  int seg = 0, prev = -1;
-  for (int r = 0; r < n; r++) {
-    const int row = order[r];
-    if (cls[row] != prev) { seg++; prev = cls[row]; }
-    keyOfRow[row] = (unsigned char)(1 + r);
-    segOfKey[1 + r] = (unsigned char)seg;
-  }
-  for (int key = n + 1; key < 64; key++) segOfKey[key] = (unsigned char)(seg + 1);
-}
-
 // Largest padded-bound coordinate of the scene, inf when a primitive has no finite bound. Every ray origin
 // is the eye or a hit point inside some padded box, so |origin| <= max(extent, |eye|) (see cullFmaOk).
 double primExtent(const std::vector<SailPrim>& prims) {
@@ -632,8 +606,6 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.cullPrims = c->n >= c->cullMinPrims ? (cullFmaOk(c) ? 2 : 1) : 0;
     A.cullPrimary = eyeNearScene(c);
     A.kernelSet = kernelSetFor(c);
-    memcpy(A.keyOfRow, c->keyOfRow, sizeof A.keyOfRow);
-    memcpy(A.segOfKey, c->segOfKey, sizeof A.segOfKey);
     memcpy(A.eye, c->eyeCache, sizeof A.eye);
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
     // = 1,016 workgroups = 4 waves per SIMD); split the launch's samples over G workgroups per block so
@@ -668,11 +640,31 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       }
       A.stage = c->stage;
     }
+    const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
+    SailWfState WS;
+    memset(&WS, 0, sizeof WS);
+    if (wavefront) {
+      A.sampleGroups = 1; A.groupSpp = nspp; A.stage = nullptr;
+      const size_t slots = (size_t)owned * 4096;
+      if (slots > c->wfSlots) {
+        if (c->wf) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->wf)); c->wf = nullptr; }
+        c->wfSlots = 0;
+        if (hipMalloc(&c->wf, slots * 11 * sizeof(float4)) != hipSuccess) { c->wf = nullptr; return fail(c, SAIL_E_OOM, "wavefront state"); }
+        c->wfSlots = slots;
+      }
+      float4* b = c->wf;
+      WS.o = b; WS.d = b + c->wfSlots; WS.f = b + 2 * c->wfSlots; WS.e = b + 3 * c->wfSlots; WS.s = b + 4 * c->wfSlots;
+      for (int i = 0; i < 6; i++) WS.sp[i] = b + (5 + i) * c->wfSlots;
+    }
     hipEvent_t e0, e1;
     if ((rc = getEvent(c, &e0)) || (rc = getEvent(c, &e1))) return rc;
     HIPCHK(c, hipEventRecord(e0, c->stream));
-    HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
-    if (A.sampleGroups > 1) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
+    if (wavefront) {
+      HIPCHK(c, sail_launch_wavefront(A, WS, c->stream));
+    } else {
+      HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
+      if (A.sampleGroups > 1) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
+    }
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending.emplace_back(e0, e1);
     c->launches++;
@@ -910,7 +902,7 @@ void sail_destroy(sail_ctx* c) {
   if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
   for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->evPool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->accum, c->frame, c->frameN, c->frameP, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples};
+  void* bufs[] = {c->accum, c->frame, c->frameN, c->frameP, c->aovN, c->aovP, c->filterOut, c->filterOut8, c->stage, c->segCounter, c->prims, c->tp, c->lt, c->lightObjRow, c->samples, c->wf};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (c->samplesPinned) (void)hipHostFree(c->samplesPinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -994,6 +986,7 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_FORCE_GENERIC: c->forceGeneric = value; break;
     case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
+    case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
     default: return fail(c, SAIL_E_INVALID, "sail_set_debug: unknown option %d", option);
   }
   return SAIL_OK;
@@ -1037,7 +1030,6 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
   c->primExtent = primExtent(prims);
-  shadeClasses(prims, c->keyOfRow, c->segOfKey);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -1081,7 +1073,6 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, c->tpRows.data(), c->tn);
   c->primExtent = primExtent(prims);
-  shadeClasses(prims, c->keyOfRow, c->segOfKey);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -71,10 +71,17 @@ struct SailTraceArgs {
   int sampleGroups, groupSpp;
   float4* stage;
   long long stageStride;    // slots per sample = ownedTiles * 4096
-  // task layout of the sorted paths (traceTileTasks, scenes of < 64 rows): each row's sort key (1 + its position in
-  // the rows ordered by shading class) and each key's class; a class starts a new wave (sail_capi.cpp shadeClasses)
-  unsigned char keyOfRow[64];
-  unsigned char segOfKey[64];
+};
+
+// Wavefront split of the pre-cull path (study switch SAIL_DEBUG_WAVEFRONT): the path state of one sample of every
+// owned pixel in HBM, one float4 array per field, slot = owned tile * 4096 + local y * 64 + local x
+struct SailWfState {
+  float4* o;     // ray origin, w = 1 while the path is alive
+  float4* d;     // ray direction
+  float4* f;     // throughput
+  float4* e;     // radiance
+  float4* s;     // sweep result: t, winning row (int bits)
+  float4* sp[6]; // a deferred shadow test: hit (w = 1 when pending), toLight, contribution, f, emission, throughput
 };
 
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a

@@ -14,14 +14,3 @@ __device__ __forceinline__ int waveScanIncl(int x) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31 -> rows 2, 3
   return v;
 }
-// Wave64 inclusive running maximum by the same DPP pattern (x >= 0: the 0 shifted in at row edges is neutral)
-__device__ __forceinline__ int waveScanMaxIncl(int x) {
-  int v = x;
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
-  return v;
-}

@@ -1481,7 +1481,16 @@ D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, float4* aovN, float4*
 }
 
 // shade() (path.glsl:1-14) + the bounce bookkeeping of trace() (path.glsl:27-36): radiance, throughput, next ray
+// A lit matte path's light sample whose shadow test is left to a later pass (the wavefront split, SAIL_DEBUG_WAVEFRONT):
+// everything the radiance update e += (emission + light * f) * fpdf needs once the shadow ray's answer is known
+struct ShadowPending { bool pending; V3 contrib, toLight, hit, f, emission, fpdfOld; };
+template <bool DEFER>
+D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, ShadowPending* sp);
 D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc) {
+  shadeBounceT<false>(c, ins, ray, seed, fpdf, e, pc, nullptr);
+}
+template <bool DEFER>
+D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, ShadowPending* sp) {
   {
     // shade()
     // box faces have axis-aligned unit dpdu: dot == 1 exactly, sqrt(1) == 1 and v / 1 == v bit for bit
@@ -1523,15 +1532,29 @@ D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf,
 #endif
     PHASE_MARK(pc, 4);  // BSDF sample
     V3 direct = v3s(0.0f);
+    bool deferE = false;
+    if (DEFER) sp->pending = false;
     if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) {
-      if (c.kLights == 0)  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
+      if (c.kLights == 0) {  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
         direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
-      else
+      } else if (DEFER) {  // lightSample's light prep now, its shadow test and the radiance update in the shadow pass
+        const LightPrep lp = lightPrep(c, ins, u2);
+        if (lp.lit) {
+          sp->pending = true; sp->contrib = lp.contrib; sp->toLight = lp.toLight; sp->hit = ins.hit; sp->f = f;
+          sp->emission = ins.emission; sp->fpdfOld = fpdf;
+          deferE = true;
+        } else {
+          direct = direct + v3s(0.0f) * f;
+        }
+      } else {
         direct = direct + lightSample(c, ins, u2) * f;
+      }
     }
     PHASE_MARK(pc, 5);  // light sample + shadow ray
-    const V3 sh = ins.emission + direct;
-    e = e + sh * fpdf;
+    if (!deferE) {
+      const V3 sh = ins.emission + direct;
+      e = e + sh * fpdf;
+    }
     fpdf = fpdf * _fpdf;
 #if SAIL_AXIS_FRAME
     const float outdot = ins.axis ? dotX(ins.normal, wi) : dot(ins.normal, wi);
@@ -1709,9 +1732,13 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_PRIO_MIXED
 #define SAIL_PRIO_MIXED 0
 #endif
-// SAIL_STATE_PACK: the migrated path state as six float2 (ds_*_b64) with the local hit point recomputed (study switch)
+// SAIL_STATE_PACK: the migrated path state as six float2 (1, ds_*_b64) or three float4 (2, ds_*_b128), the local hit
+// point recomputed; SAIL_E4: each pixel's radiance slot as one float4
 #ifndef SAIL_STATE_PACK
 #define SAIL_STATE_PACK 0
+#endif
+#ifndef SAIL_E4
+#define SAIL_E4 0
 #endif
 // the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
 #ifndef SAIL_SCAN_DPP
@@ -1740,7 +1767,13 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
-#if SAIL_STATE_PACK
+#if SAIL_STATE_PACK == 2
+  // packed path state: three float4 per path -- ray o + d.x, d.yz + throughput.xy, throughput.z + distance + pixel |
+  // row << 10 (ds_write_b128 / ds_read_b128: 3 + 3 LDS instructions instead of 15 + 15); the local hit point is
+  // recomputed (hitRecord<true>)
+  __shared__ float4 sSt4[3][NT];
+  (void)kFields;
+#elif SAIL_STATE_PACK
   // packed path state: six float2 per path, ray o / d, throughput, distance, pixel | row << 10 (ds_write_b64 /
   // ds_read_b64: 6 + 6 LDS instructions instead of 15 + 15); the local hit point is recomputed (hitRecord<true>)
   __shared__ float2 sSt2[6][NT];
@@ -1748,7 +1781,15 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #else
   __shared__ float sSt[kFields][NT];
 #endif
+#if SAIL_E4
+  __shared__ float4 sE4[NT];  // each pixel's radiance as one float4 (one ds_read_b128 / ds_write_b128)
+#define E_LOAD(i) v3(sE4[i].x, sE4[i].y, sE4[i].z)
+#define E_STORE(i, v) (sE4[i] = make_float4((v).x, (v).y, (v).z, 0.0f))
+#else
   __shared__ float sE[3][NT];
+#define E_LOAD(i) v3(sE[0][i], sE[1][i], sE[2][i])
+#define E_STORE(i, v) (sE[0][i] = (v).x, sE[1][i] = (v).y, sE[2][i] = (v).z)
+#endif
   constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
@@ -1807,11 +1848,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   // sample kPrev's radiance into the accumulator / stage; a path that missed at once (dead) clears its slot
   auto settlePrev = [&](bool alive) {
     if (valid && kPrev >= 0) {
-      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
+      const V3 er = E_LOAD(li);
       if (grouped) stageSample<NT>(A, kPrev, tw.bid, li, er);
       else accumulateSample(acc, er, constRow<SailSample>(A.samples, kPrev), A.accumMode);
     }
-    if (!alive) { sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f; }
+    if (!alive) E_STORE(li, v3s(0.0f));
   };
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = constRow<SailSample>(A.samples, k);
@@ -1826,7 +1867,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     }
     V3 fpdf = v3s(1.0f);
     // the path's radiance lives in LDS at its pixel: one path per pixel, updated in bounce order
-    if (!deferRead) { sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f; }
+    if (!deferRead) E_STORE(li, v3s(0.0f));
     for (int depth = 1; depth <= A.maxBounces; depth++) {
       Sweep sw;
       sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
@@ -1861,10 +1902,14 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int nAlive;
       // a path's state into sorted slot d
       auto scatterTo = [&](int d) {
-#if SAIL_STATE_PACK
+#if SAIL_STATE_PACK == 2
+        sSt4[0][d] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
+        sSt4[1][d] = make_float4(ray.d.y, ray.d.z, fpdf.x, fpdf.y);
+        sSt4[2][d] = make_float4(fpdf.z, sw.best, __int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
+#elif SAIL_STATE_PACK
         sSt2[0][d] = make_float2(ray.o.x, ray.o.y); sSt2[1][d] = make_float2(ray.o.z, ray.d.x);
         sSt2[2][d] = make_float2(ray.d.y, ray.d.z); sSt2[3][d] = make_float2(fpdf.x, fpdf.y);
-        sSt2[4][d] = make_float2(fpdf.z, sw.best); sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), 0.0f);
+        sSt2[4][d] = make_float2(fpdf.z, sw.best); sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
 #else
         sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
         sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
@@ -1924,12 +1969,29 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       __syncthreads();
       }
       alive = li < nAlive;
+      int keyG = 0;  // the gathered path's sort key (packed state only)
+      (void)keyG;
       PHASE_MARK(pc, 7);
       if (alive) {
-#if SAIL_STATE_PACK
+#if SAIL_STATE_PACK == 2
+        {
+          const float4 q0 = sSt4[0][li], q1 = sSt4[1][li], q2 = sSt4[2][li];
+          const int pk = __float_as_int(q2.z);
+          keyG = __float_as_int(q2.w);
+          ray.o = v3(q0.x, q0.y, q0.z);
+          ray.d = v3(q0.w, q1.x, q1.y);
+          fpdf = v3(q1.z, q1.w, q2.x);
+          sw.best = q2.y;
+          pixel = pk & 1023;
+          sw.bi = pk >> 10;
+          sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
+        }
+        ray.rx = ray.ry = ray.rz = 0.0f;
+#elif SAIL_STATE_PACK
         {
           const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
           const int pk = __float_as_int(sSt2[5][li].x);
+          keyG = __float_as_int(sSt2[5][li].y);
           ray.o = v3(q0.x, q0.y, q1.x);
           ray.d = v3(q1.y, q2.x, q2.y);
           fpdf = v3(q3.x, q3.y, q4.x);
@@ -1949,10 +2011,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
 #endif
 #if SAIL_PRIO_MIXED
-        {  // a wave whose live paths won different rows runs several hit-record / material branches: raise its issue
-           // priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
-          const int b0 = __builtin_amdgcn_readfirstlane(sw.bi);
-          if (__builtin_amdgcn_ballot_w64(sw.bi != b0) != 0ull) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
+        {  // a wave whose live paths have different sort keys runs several hit-record / material branches: raise its
+           // issue priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
+          const int kk = SAIL_STATE_PACK ? keyG : sw.bi;
+          const int k0 = __builtin_amdgcn_readfirstlane(kk);
+          if (__builtin_amdgcn_ballot_w64(kk != k0) != 0ull) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
           else __builtin_amdgcn_s_setprio(0);
         }
 #endif
@@ -1966,16 +2029,16 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
-        V3 e = (deferRead && depth == 1) ? v3s(0.0f) : v3(sE[0][pixel], sE[1][pixel], sE[2][pixel]);
+        V3 e = (deferRead && depth == 1) ? v3s(0.0f) : E_LOAD(pixel);
         if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
           shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
-        sE[0][pixel] = e.x; sE[1][pixel] = e.y; sE[2][pixel] = e.z;
+        E_STORE(pixel, e);
       }
     }
     if (deferRead) { kPrev = k; continue; }
     __syncthreads();
     if (valid) {
-      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
+      const V3 er = E_LOAD(li);
       if (grouped) stageSample<NT>(A, k, tw.bid, li, er);
       else accumulateSample(acc, er, S, A.accumMode);
     }
@@ -1996,206 +2059,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
   }
 }
-// ---- task layout of the sorted paths (SAIL_ROOM_TILE=traceTileTasks) -------------------------------------------------
-// traceTileCompact packs the sorted paths contiguously, so the few paths of each small key share the workgroup's last
-// wave: in the C3 room that wave runs the metal, mirror, glass and lit-matte branches one after another while the
-// other waves wait at the next barrier. Here the sorted order is laid out in 64-slot "tasks": each shading class (the
-// rows' material, and whether they emit, sail_capi.cpp shadeClasses) starts a new task, so a task holds paths of one
-// class, and the waves take the tasks round robin (up to kMaxTasks: several per wave). Each path keeps a home slot
-// (its pixel's lane): the home lane sweeps the path's ray (dense, every lane of a wave busy) and counts its key; the
-// sorted order is a permutation of home slots, and the task lanes read the path's state from its home slot, shade it
-// and write the next ray back home. Three barriers per bounce; no end-of-sample barriers (a pixel's radiance slot is
-// its home lane's). Only the lane that shades a path changes: the result is bit-identical.
-template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
-__device__ __forceinline__ void traceTileTasks(const SailTraceArgs& A) {
-  static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
-  constexpr int NW = NT / 64;
-  constexpr int kKeys = 64;
-  constexpr int kMaxTasks = 3 * NW;        // room for every class to start its own task, up to 3 rounds
-  // home state: ray o, d (0..5), throughput (6..8), winning row (9), distance (10), local hit point (11..13)
-  __shared__ float sSt[14][NT];
-  __shared__ float sE[3][NT];
-  __shared__ int sCnt[kKeys];
-  __shared__ short sPerm[kMaxTasks * 64];
-  const TileWork tw = tileWork<GROUPED, NT>(A);
-  const int ownedTile = tw.ownedTile;
-  if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
-  const int sub = tw.sub;
-  const int tile = A.rank + ownedTile * A.world;
-  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
-  const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
-  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * (NT / 16);
-  const int x = x0 + (li & 15), y = y0 + (li >> 4);
-  const bool valid = x < A.W && y < A.H;
-
-  Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
-  c.prims = A.prims;
-  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
-  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
-  c.fcx = 0.0f; c.fcy = 0.0f;
-  c.shadowAnyHit = A.shadowAnyHit;
-  c.cullPrims = CULL ? 1 : 0;
-  c.cullFma = CULL && A.cullPrims == 2;
-  c.cullPrimary = A.cullPrimary;
-  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
-
-  if (li < kKeys) sCnt[li] = 0;
-  // rows -> keys in shading-class order (host tables) when the scene has few rows, else (material, shape)
-  const bool byPrim = A.n < kKeys;
-  // this lane's key (= lane) and its class; a class's first key starts a task
-  const int segL = byPrim ? (int)A.segOfKey[lane] : (lane + 9) / 10;
-  const int segNext = lane == 63 ? -1 : (byPrim ? (int)A.segOfKey[lane + 1] : (lane + 10) / 10);
-  const bool firstOfSeg = lane == 0 || segL != (byPrim ? (int)A.segOfKey[lane - 1] : (lane + 8) / 10);
-  const bool lastOfSeg = segNext != segL;
-  __syncthreads();
-  const size_t pixG = (size_t)y * A.W + x;
-  constexpr bool grouped = GROUPED;
-  float4 acc = (valid && !grouped) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
-  const bool tri0 = s + t <= 1.0f;
-  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
-  unsigned segs = 0;
-  PhaseClock pc;
-#if SAIL_PHASE_TIMING
-  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
-  pc.t = __builtin_amdgcn_s_memtime();
-#endif
-  for (int k = tw.kBeg; k < tw.kEnd; k++) {
-    const SailSample& S = constRow<SailSample>(A.samples, k);
-    const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
-    bool alive = valid;
-    // the path's radiance lives in LDS at its pixel (its home lane), updated in bounce order
-    sE[0][li] = 0.0f; sE[1][li] = 0.0f; sE[2][li] = 0.0f;
-    for (int depth = 1; depth <= A.maxBounces; depth++) {
-      // ---- phase A (home lane): the path's sweep and its key
-      int key = 0;
-      if (alive) {
-        Ray ray;
-        if (depth == 1) {
-          const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
-          const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
-          ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
-          sSt[0][li] = ray.o.x; sSt[1][li] = ray.o.y; sSt[2][li] = ray.o.z;
-          sSt[3][li] = ray.d.x; sSt[4][li] = ray.d.y; sSt[5][li] = ray.d.z;
-          sSt[6][li] = 1.0f; sSt[7][li] = 1.0f; sSt[8][li] = 1.0f;
-        } else {
-          ray = mkRay(v3(sSt[0][li], sSt[1][li], sSt[2][li]), v3(sSt[3][li], sSt[4][li], sSt[5][li]));
-        }
-        segs++;
-        const Sweep sw = sweepRay(c, ray, depth == 1);
-        if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
-          if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
-            const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
-            if (A.aovN) A.aovN[pixG] = make_float4(qn.x, qn.y, qn.z, 1.0f);
-            if (A.aovP) A.aovP[pixG] = make_float4(qp.x, qp.y, qp.z, 1.0f);
-          }
-          alive = false;
-        } else {
-          if (byPrim) {
-            key = (int)A.keyOfRow[sw.bi];
-          } else {
-            const SailPrim& p = PRIM(c, sw.bi);
-            int mc = matCat(p);
-            mc = (mc >= 0 && mc < 5) ? mc : 0;
-            key = 1 + mc * 10 + p.type;
-          }
-          sSt[9][li] = __int_as_float(sw.bi); sSt[10][li] = sw.best;
-          sSt[11][li] = sw.bhl.x; sSt[12][li] = sw.bhl.y; sSt[13][li] = sw.bhl.z;
-        }
-      }
-      PHASE_MARK(pc, 0);
-      const int rank = alive ? atomicAdd(&sCnt[key], 1) : 0;
-      __syncthreads();  // B1: counts complete, home state written
-      // ---- every wave lays out the sorted order itself: key starts, each class padded to start a new task
-      int nTasks, nAlive;
-      bool padded;
-      int classEnd, classInfo;  // at a class's last key: its padded end, and (path count | padded size << 16)
-      {
-        const int v = sCnt[lane];
-        const int incl = waveScanIncl(v);
-        const int excl = incl - v;
-        nAlive = __builtin_amdgcn_readlane(incl, 63);
-        const int base = waveScanMaxIncl(firstOfSeg ? excl : 0);  // unpadded start of this key's class
-        const int total = incl - base;                              // at the class's last key: the class size
-        const int R = lastOfSeg ? ((total + 63) & ~63) : 0;
-        const int Rincl = waveScanIncl(R);
-        const int paddedTotal = __builtin_amdgcn_readlane(Rincl, 63);
-        padded = paddedTotal <= kMaxTasks * 64;
-        nTasks = padded ? paddedTotal >> 6 : (nAlive + 63) >> 6;
-        const int keyStart = padded ? (Rincl - R) + (excl - base) : excl;
-        classEnd = lastOfSeg ? Rincl : -1;  // only a class's last key is a candidate of the per-task search
-        classInfo = lastOfSeg ? (total | (R << 16)) : 0;
-        const int start = __shfl(keyStart, key, 64);
-        if (alive) sPerm[start + rank] = (short)li;
-      }
-      __syncthreads();  // B2: the permutation is complete; counts read by every wave
-      if (wave == 0) sCnt[lane] = 0;
-      PHASE_MARK(pc, 7);
-      // ---- phase B (task lanes): hit record and shading of the path in each of this wave's task slots
-      for (int tk = wave; tk < nTasks; tk += NW) {
-        const int slot = tk * 64 + lane;
-        bool on;
-        if (padded) {
-          // the class holding this task: the first class (last-key lane) whose padded end lies beyond the task start
-          const unsigned long long m = __builtin_amdgcn_ballot_w64(classEnd > tk * 64);
-          const int L = (int)__builtin_ctzll(m);
-          const int endL = __builtin_amdgcn_readlane(classEnd, L);
-          const int info = __builtin_amdgcn_readlane(classInfo, L);
-          on = slot - (endL - (info >> 16)) < (info & 0xffff);
-        } else {
-          on = slot < nAlive;
-        }
-        if (!on) continue;
-        const int p = (int)sPerm[slot] & (NT - 1);  // a home slot (the mask keeps every access in bounds regardless)
-        Ray ray;
-        ray.o = v3(sSt[0][p], sSt[1][p], sSt[2][p]);
-        ray.d = v3(sSt[3][p], sSt[4][p], sSt[5][p]);
-        ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
-        V3 fpdf = v3(sSt[6][p], sSt[7][p], sSt[8][p]);
-        Sweep sw;
-        sw.bi = __float_as_int(sSt[9][p]); sw.best = sSt[10][p];
-        sw.bhl = v3(sSt[11][p], sSt[12][p], sSt[13][p]);
-        c.fcx = (float)(x0 + (p & 15)) + 0.5f;
-        c.fcy = (float)(y0 + (p >> 4)) + 0.5f;
-        const Hit ins = hitRecordU(c, ray, sw);
-        PHASE_MARK(pc, 1);
-        if (depth == 1 && aovSample && x0 + (p & 15) < A.W && y0 + (p >> 4) < A.H) {
-          const size_t g = (size_t)(y0 + (p >> 4)) * A.W + x0 + (p & 15);
-          const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
-          if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
-          if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
-        }
-        V3 e = v3(sE[0][p], sE[1][p], sE[2][p]);
-        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
-          shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
-        sE[0][p] = e.x; sE[1][p] = e.y; sE[2][p] = e.z;
-        if (depth < A.maxBounces) {
-          sSt[0][p] = ray.o.x; sSt[1][p] = ray.o.y; sSt[2][p] = ray.o.z;
-          sSt[3][p] = ray.d.x; sSt[4][p] = ray.d.y; sSt[5][p] = ray.d.z;
-          sSt[6][p] = fpdf.x; sSt[7][p] = fpdf.y; sSt[8][p] = fpdf.z;
-        }
-      }
-      __syncthreads();  // B3: next rays and radiance written
-    }
-    if (valid) {
-      const V3 er = v3(sE[0][li], sE[1][li], sE[2][li]);
-      if (grouped) stageSample<NT>(A, k, tw.bid, li, er);
-      else accumulateSample(acc, er, S, A.accumMode);
-    }
-  }
-  if (valid && !grouped) A.accum[pixG] = acc;
-#if SAIL_PHASE_TIMING
-  if (lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
-#endif
-  if (A.segCounter) {
-    unsigned long long v = segs;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * (unsigned)NW + (unsigned)wave) % SAIL_SEG_SLOTS], v);
-  }
-}
-
 // Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;
 // earlier builds with more live state lost to spills in the flat kernels). SAIL_COMPACT=0 / SAIL_*_TILE select
 // the unsorted body for comparisons.
@@ -2271,6 +2134,161 @@ SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_RO
 #endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT,
                       SAIL_CULL_GROUP_NT)
+
+// ---- wavefront split of the pre-cull path (study switch SAIL_DEBUG_WAVEFRONT; DESIGN.md §9 of round 2) -------------------
+// The megakernel keeps each path in registers and LDS across its bounces and sorts the workgroup's paths between the
+// sweep and the shading. Here one sample of every owned pixel is traced bounce by bounce with the state in HBM and
+// four kernels per bounce pass: the sweep, the hit record + shading (a lit matte path's shadow test deferred), the
+// shadow sweep of the deferred tests with the radiance update they hold back, then (per sample) the accumulation.
+// Each kernel runs with only its own live state. Same functions, same operations in the same order: bit-identical.
+namespace {
+struct WfPix { int x, y; bool valid; };
+D WfPix wfPixel(const SailTraceArgs& A, long long slot) {
+  const int ownedTile = (int)(slot >> 12), local = (int)(slot & 4095);
+  const int tile = A.rank + ownedTile * A.world;
+  WfPix q;
+  q.x = (tile % A.tilesX) * 64 + (local & 63);
+  q.y = (tile / A.tilesX) * 64 + (local >> 6);
+  q.valid = ownedTile < A.ownedTiles && q.x < A.W && q.y < A.H;
+  return q;
+}
+D Ctx wfCtx(const SailTraceArgs& A) {
+  Ctx c;
+  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
+  c.prims = A.prims;
+  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
+  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
+  c.fcx = 0.0f; c.fcy = 0.0f;
+  c.shadowAnyHit = A.shadowAnyHit;
+  c.cullPrims = 1;
+  c.cullFma = A.cullPrims == 2;
+  c.cullPrimary = A.cullPrimary;
+  c.kShapes = ~0u; c.kMats = ~0u; c.kTex = ~0u; c.kLights = ~0u;
+  return c;
+}
+}  // namespace
+// primary rays of sample k
+extern "C" __global__ void __launch_bounds__(256) sail_wf_primary(SailTraceArgs A, SailWfState S, int k) {
+  const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
+  const WfPix q = wfPixel(A, slot);
+  const SailSample& sm = constRow<SailSample>(A.samples, k);
+  const float s = ((float)q.x + 0.5f) / (float)A.W, t = ((float)q.y + 0.5f) / (float)A.H;
+  const V3 d0 = v3(sm.d[0][0], sm.d[0][1], sm.d[0][2]), d1 = v3(sm.d[1][0], sm.d[1][1], sm.d[1][2]);
+  const V3 d2 = v3(sm.d[2][0], sm.d[2][1], sm.d[2][2]), d3 = v3(sm.d[3][0], sm.d[3][1], sm.d[3][2]);
+  const V3 dir = (s + t <= 1.0f) ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t));
+  S.o[slot] = make_float4(A.eye[0], A.eye[1], A.eye[2], q.valid ? 1.0f : 0.0f);
+  S.d[slot] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+  S.f[slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+  S.e[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+// the closest-hit sweep of every live path
+extern "C" __global__ void __launch_bounds__(256) sail_wf_sweep(SailTraceArgs A, SailWfState S, int k, int depth) {
+  const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
+  const float4 o = S.o[slot];
+  unsigned seg = 0;
+  if (o.w != 0.0f) {
+    const Ctx c = wfCtx(A);
+    const float4 d = S.d[slot];
+    const Ray ray = mkRay(v3(o.x, o.y, o.z), v3(d.x, d.y, d.z));
+    const Sweep sw = sweepRay(c, ray, depth == 1);
+    seg = 1;
+    if (sw.best >= kMaxDistance) {  // the path leaves the scene
+      S.o[slot] = make_float4(o.x, o.y, o.z, 0.0f);
+      if (depth == 1 && (A.aovN || A.aovP) && k == A.spp - 1) {
+        const WfPix q = wfPixel(A, slot);
+        const size_t g = (size_t)q.y * A.W + q.x;
+        const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
+        if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+        if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+      }
+    } else {
+      S.s[slot] = make_float4(sw.best, __int_as_float(sw.bi), 0.0f, 0.0f);
+    }
+  }
+  if (A.segCounter) {
+    unsigned long long v = seg;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (threadIdx.x >> 6)) % SAIL_SEG_SLOTS], v);
+  }
+}
+// hit record and shading of every live path; a lit matte path's shadow test and radiance update are deferred
+extern "C" __global__ void __launch_bounds__(256) sail_wf_shade(SailTraceArgs A, SailWfState S, int k, int depth) {
+  const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
+  const float4 o = S.o[slot];
+  if (o.w == 0.0f) { S.sp[0][slot].w = 0.0f; return; }
+  Ctx c = wfCtx(A);
+  const WfPix q = wfPixel(A, slot);
+  c.fcx = (float)q.x + 0.5f; c.fcy = (float)q.y + 0.5f;
+  const float4 d = S.d[slot], fp = S.f[slot], ee = S.e[slot], sv = S.s[slot];
+  Ray ray;
+  ray.o = v3(o.x, o.y, o.z); ray.d = v3(d.x, d.y, d.z); ray.rx = ray.ry = ray.rz = 0.0f;
+  Sweep sw;
+  sw.best = sv.x; sw.bi = __float_as_int(sv.y); sw.bhl = v3s(0.0f);
+  const Hit ins = hitRecord<true>(c, ray, sw);
+  if (depth == 1 && (A.aovN || A.aovP) && k == A.spp - 1) {
+    const size_t g = (size_t)q.y * A.W + q.x;
+    const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
+    if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
+    if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
+  }
+  V3 fpdf = v3(fp.x, fp.y, fp.z), e = v3(ee.x, ee.y, ee.z);
+  const float seed = constRow<SailSample>(A.samples, k).seed + (float)depth;
+  PhaseClock pc;
+  ShadowPending sp;
+  shadeBounceT<true>(c, ins, ray, seed, fpdf, e, pc, &sp);
+  S.e[slot] = make_float4(e.x, e.y, e.z, 0.0f);
+  S.f[slot] = make_float4(fpdf.x, fpdf.y, fpdf.z, 0.0f);
+  S.o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, 1.0f);
+  S.d[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+  S.sp[0][slot] = make_float4(sp.hit.x, sp.hit.y, sp.hit.z, sp.pending ? 1.0f : 0.0f);
+  if (sp.pending) {
+    S.sp[1][slot] = make_float4(sp.toLight.x, sp.toLight.y, sp.toLight.z, 0.0f);
+    S.sp[2][slot] = make_float4(sp.contrib.x, sp.contrib.y, sp.contrib.z, 0.0f);
+    S.sp[3][slot] = make_float4(sp.f.x, sp.f.y, sp.f.z, 0.0f);
+    S.sp[4][slot] = make_float4(sp.emission.x, sp.emission.y, sp.emission.z, 0.0f);
+    S.sp[5][slot] = make_float4(sp.fpdfOld.x, sp.fpdfOld.y, sp.fpdfOld.z, 0.0f);
+  }
+}
+// the deferred shadow tests (testShadow, shader.light.js:24-31) and the radiance update they held back:
+// direct = 0 + light * f, e = e + (emission + direct) * throughput, as shadeBounce writes it
+extern "C" __global__ void __launch_bounds__(256) sail_wf_shadow(SailTraceArgs A, SailWfState S) {
+  const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
+  const float4 h = S.sp[0][slot];
+  if (h.w == 0.0f) return;
+  const Ctx c = wfCtx(A);
+  const float4 tl = S.sp[1][slot], ct = S.sp[2][slot], ff = S.sp[3][slot], em = S.sp[4][slot], fo = S.sp[5][slot];
+  const V3 light = testShadow(c, mkRay(v3(h.x, h.y, h.z), v3(tl.x, tl.y, tl.z))) ? v3s(0.0f) : v3(ct.x, ct.y, ct.z);
+  V3 direct = v3s(0.0f);
+  direct = direct + light * v3(ff.x, ff.y, ff.z);
+  const V3 sh = v3(em.x, em.y, em.z) + direct;
+  const float4 ee = S.e[slot];
+  const V3 e = v3(ee.x, ee.y, ee.z) + sh * v3(fo.x, fo.y, fo.z);
+  S.e[slot] = make_float4(e.x, e.y, e.z, 0.0f);
+}
+// sample k's radiance into the accumulator (sample order: one launch per sample)
+extern "C" __global__ void __launch_bounds__(256) sail_wf_accum(SailTraceArgs A, SailWfState S, int k) {
+  const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
+  const WfPix q = wfPixel(A, slot);
+  if (!q.valid) return;
+  const size_t pix = (size_t)q.y * A.W + q.x;
+  float4 acc = A.accum[pix];
+  const float4 ee = S.e[slot];
+  accumulateSample(acc, v3(ee.x, ee.y, ee.z), constRow<SailSample>(A.samples, k), A.accumMode);
+  A.accum[pix] = acc;
+}
+hipError_t sail_launch_wavefront(const SailTraceArgs& A, const SailWfState& S, hipStream_t s) {
+  const unsigned blocks = (unsigned)A.ownedTiles * 16u;  // 4096 slots per owned tile, 256 per workgroup
+  for (int k = 0; k < A.spp; k++) {
+    hipLaunchKernelGGL(sail_wf_primary, dim3(blocks), dim3(256), 0, s, A, S, k);
+    for (int depth = 1; depth <= A.maxBounces; depth++) {
+      hipLaunchKernelGGL(sail_wf_sweep, dim3(blocks), dim3(256), 0, s, A, S, k, depth);
+      hipLaunchKernelGGL(sail_wf_shade, dim3(blocks), dim3(256), 0, s, A, S, k, depth);
+      hipLaunchKernelGGL(sail_wf_shadow, dim3(blocks), dim3(256), 0, s, A, S);
+    }
+    hipLaunchKernelGGL(sail_wf_accum, dim3(blocks), dim3(256), 0, s, A, S, k);
+  }
+  return hipGetLastError();
+}
 
 // ---- sample groups: add the staged per-sample radiance to the accumulator in sample order ---------------------
 extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArgs A) {

@@ -358,6 +358,18 @@ def test_kernel_selection(gpu, fixtures):
         ctx.close()
 
 
+# ---- the wavefront split of the pre-cull path (study switch): bit-identical to the megakernel and the oracle ------
+@pytest.mark.parametrize("name,W,H,spp,B,mode", [("C4", 70, 46, 3, 12, capi.ACCUM_SUM), ("ALL", 40, 32, 4, 6, capi.ACCUM_MIX),
+                                                 ("AREA", 36, 30, 3, 5, capi.ACCUM_SUM), ("C3", 40, 40, 3, 8, capi.ACCUM_COMPAT8)])
+def test_wavefront_split_bit_exact(gpu, fixtures, monkeypatch, name, W, H, spp, B, mode):
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_WAVEFRONT, 1)
+    monkeypatch.setitem(capi.DEBUG_DEFAULTS, capi.DEBUG_CULL_MIN_PRIMS, 0)  # every scene on the pre-cull path
+    got, want, st, segs, gaov, waov = _render_both(fixtures, name, W, H, spp, B, mode=mode, aov=True, launch=2)
+    assert bit_equal(got, want).all()
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
+
+
 # ---- sample groups (small per-rank frames): staged samples added in order are bit-identical ---------------------
 @pytest.mark.parametrize("groups", [0, 3, 4])
 @pytest.mark.parametrize("rank,world", [(0, 1), (1, 3)])
