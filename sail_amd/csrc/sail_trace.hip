@@ -1728,17 +1728,27 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_MATMAJOR
 #define SAIL_SORT_MATMAJOR 1
 #endif
-// SAIL_PRIO_MIXED = p: after the sort, a wave whose paths won different rows runs at issue priority p (study switch)
+// SAIL_PRIO_MIXED = p: after the sort, a wave whose live paths have different sort keys runs at issue priority p
+// (variants in gpurun_out/r03f: C3 +7.3 % alone)
 #ifndef SAIL_PRIO_MIXED
-#define SAIL_PRIO_MIXED 0
+#define SAIL_PRIO_MIXED 2
 #endif
-// SAIL_STATE_PACK: the migrated path state as six float2 (1, ds_*_b64) or three float4 (2, ds_*_b128), the local hit
-// point recomputed; SAIL_E4: each pixel's radiance slot as one float4
+// SAIL_STATE_PACK (SAIL_STATE_PACK_CULL for the pre-cull kernel): the migrated path state as 15 floats (0), six float2
+// (1, ds_*_b64) or three float4 (2, ds_*_b128), the local hit point recomputed when packed; SAIL_E4 (_CULL): each
+// pixel's radiance slot as one float4. Measured with priority 2 (gpurun_out/r03g, Gseg/s C1 / C3 / C4): pack 1
+// 89.6 / 29.0 / 9.40, pack 2 90.0 / 29.0 / 9.10, pack 1 + E4 90.1 / 29.15 / 9.10, pack 2 + E4 90.3 / 29.15 / 9.10
+// (no packing, no priority: 86.0 / 26.3 / 9.04)
 #ifndef SAIL_STATE_PACK
-#define SAIL_STATE_PACK 0
+#define SAIL_STATE_PACK 2
 #endif
 #ifndef SAIL_E4
-#define SAIL_E4 0
+#define SAIL_E4 1
+#endif
+#ifndef SAIL_STATE_PACK_CULL
+#define SAIL_STATE_PACK_CULL 1
+#endif
+#ifndef SAIL_E4_CULL
+#define SAIL_E4_CULL 0
 #endif
 // the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
 #ifndef SAIL_SCAN_DPP
@@ -1767,29 +1777,25 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kFields = 15;
-#if SAIL_STATE_PACK == 2
-  // packed path state: three float4 per path -- ray o + d.x, d.yz + throughput.xy, throughput.z + distance + pixel |
-  // row << 10 (ds_write_b128 / ds_read_b128: 3 + 3 LDS instructions instead of 15 + 15); the local hit point is
-  // recomputed (hitRecord<true>)
-  __shared__ float4 sSt4[3][NT];
-  (void)kFields;
-#elif SAIL_STATE_PACK
-  // packed path state: six float2 per path, ray o / d, throughput, distance, pixel | row << 10 (ds_write_b64 /
-  // ds_read_b64: 6 + 6 LDS instructions instead of 15 + 15); the local hit point is recomputed (hitRecord<true>)
-  __shared__ float2 sSt2[6][NT];
-  (void)kFields;
-#else
-  __shared__ float sSt[kFields][NT];
-#endif
-#if SAIL_E4
-  __shared__ float4 sE4[NT];  // each pixel's radiance as one float4 (one ds_read_b128 / ds_write_b128)
-#define E_LOAD(i) v3(sE4[i].x, sE4[i].y, sE4[i].z)
-#define E_STORE(i, v) (sE4[i] = make_float4((v).x, (v).y, (v).z, 0.0f))
-#else
-  __shared__ float sE[3][NT];
-#define E_LOAD(i) v3(sE[0][i], sE[1][i], sE[2][i])
-#define E_STORE(i, v) (sE[0][i] = (v).x, sE[1][i] = (v).y, sE[2][i] = (v).z)
-#endif
+  constexpr int kPack = CULL ? SAIL_STATE_PACK_CULL : SAIL_STATE_PACK;
+  constexpr bool kE4 = CULL ? SAIL_E4_CULL : SAIL_E4;
+  // packed path state, 2: three float4 per path -- ray o + d.x, d.yz + throughput.xy, throughput.z + distance +
+  // pixel | row << 10 + key (ds_write_b128 / ds_read_b128: 3 + 3 LDS instructions instead of 15 + 15); 1: six
+  // float2 (ds_*_b64); the local hit point is recomputed (hitRecord<true>). Unused forms are one element.
+  __shared__ float4 sSt4[kPack == 2 ? 3 : 1][kPack == 2 ? NT : 1];
+  __shared__ float2 sSt2[kPack == 1 ? 6 : 1][kPack == 1 ? NT : 1];
+  __shared__ float sSt[kPack == 0 ? kFields : 1][kPack == 0 ? NT : 1];
+  // each pixel's radiance: one float4 (one ds_read_b128 / ds_write_b128) or three floats
+  __shared__ float4 sE4[kE4 ? NT : 1];
+  __shared__ float sE[kE4 ? 1 : 3][kE4 ? 1 : NT];
+  auto E_LOAD = [&](int i) -> V3 {
+    if constexpr (kE4) return v3(sE4[i].x, sE4[i].y, sE4[i].z);
+    else return v3(sE[0][i], sE[1][i], sE[2][i]);
+  };
+  auto E_STORE = [&](int i, const V3& v) {
+    if constexpr (kE4) sE4[i] = make_float4(v.x, v.y, v.z, 0.0f);
+    else { sE[0][i] = v.x; sE[1][i] = v.y; sE[2][i] = v.z; }
+  };
   constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
@@ -1902,21 +1908,22 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int nAlive;
       // a path's state into sorted slot d
       auto scatterTo = [&](int d) {
-#if SAIL_STATE_PACK == 2
-        sSt4[0][d] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
-        sSt4[1][d] = make_float4(ray.d.y, ray.d.z, fpdf.x, fpdf.y);
-        sSt4[2][d] = make_float4(fpdf.z, sw.best, __int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
-#elif SAIL_STATE_PACK
-        sSt2[0][d] = make_float2(ray.o.x, ray.o.y); sSt2[1][d] = make_float2(ray.o.z, ray.d.x);
-        sSt2[2][d] = make_float2(ray.d.y, ray.d.z); sSt2[3][d] = make_float2(fpdf.x, fpdf.y);
-        sSt2[4][d] = make_float2(fpdf.z, sw.best); sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
-#else
-        sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
-        sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
-        sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
-        sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
-        sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
-#endif
+        if constexpr (kPack == 2) {
+          sSt4[0][d] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
+          sSt4[1][d] = make_float4(ray.d.y, ray.d.z, fpdf.x, fpdf.y);
+          sSt4[2][d] = make_float4(fpdf.z, sw.best, __int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
+        } else if constexpr (kPack == 1) {
+          sSt2[0][d] = make_float2(ray.o.x, ray.o.y); sSt2[1][d] = make_float2(ray.o.z, ray.d.x);
+          sSt2[2][d] = make_float2(ray.d.y, ray.d.z); sSt2[3][d] = make_float2(fpdf.x, fpdf.y);
+          sSt2[4][d] = make_float2(fpdf.z, sw.best);
+          sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
+        } else {
+          sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
+          sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
+          sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
+          sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
+          sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
+        }
       };
       if constexpr (twoBar) {
       // every wave scans the counts itself (the start of a lane's key by a cross-lane read), so no barrier
@@ -1973,8 +1980,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       (void)keyG;
       PHASE_MARK(pc, 7);
       if (alive) {
-#if SAIL_STATE_PACK == 2
-        {
+        if constexpr (kPack == 2) {
           const float4 q0 = sSt4[0][li], q1 = sSt4[1][li], q2 = sSt4[2][li];
           const int pk = __float_as_int(q2.z);
           keyG = __float_as_int(q2.w);
@@ -1985,10 +1991,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           pixel = pk & 1023;
           sw.bi = pk >> 10;
           sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
-        }
-        ray.rx = ray.ry = ray.rz = 0.0f;
-#elif SAIL_STATE_PACK
-        {
+        } else if constexpr (kPack == 1) {
           const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
           const int pk = __float_as_int(sSt2[5][li].x);
           keyG = __float_as_int(sSt2[5][li].y);
@@ -1999,21 +2002,19 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           pixel = pk & 1023;
           sw.bi = pk >> 10;
           sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
+        } else {
+          ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
+          ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
+          fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
+          pixel = __float_as_int(sSt[9][li]);
+          sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
+          sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
         }
         ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
-#else
-        ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
-        ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
-        ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
-        fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
-        pixel = __float_as_int(sSt[9][li]);
-        sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
-        sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
-#endif
 #if SAIL_PRIO_MIXED
         {  // a wave whose live paths have different sort keys runs several hit-record / material branches: raise its
            // issue priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
-          const int kk = SAIL_STATE_PACK ? keyG : sw.bi;
+          const int kk = kPack ? keyG : sw.bi;
           const int k0 = __builtin_amdgcn_readfirstlane(kk);
           if (__builtin_amdgcn_ballot_w64(kk != k0) != 0ull) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
           else __builtin_amdgcn_s_setprio(0);
@@ -2021,7 +2022,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #endif
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
-        const Hit ins = hitRecordU<SAIL_STATE_PACK != 0>(c, ray, sw);
+        const Hit ins = hitRecordU<kPack != 0>(c, ray, sw);
         PHASE_MARK(pc, 1);
         if (depth == 1 && aovSample) {
           const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
