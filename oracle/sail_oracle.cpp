@@ -21,6 +21,7 @@
 // known-answer tests (tests/test_oracle_*.py). The GLSL itself cannot execute in this container.
 //
 // Build: oracle/build.sh -> oracle/build/libsail_oracle.so (+ libsail_oracle_count.so, SAIL_COUNT_OPS)
+#include <cstring>
 #include <stdint.h>
 #include <string.h>
 #include <math.h>
@@ -1151,6 +1152,31 @@ static F falloff(F cosTotalWidth, F cosFalloffStart, V3 w) {  // spot.glsl:17-27
   const F delta2 = delta * delta;
   return delta2 * delta2;
 }
+#ifdef SAIL_COUNT_OPS
+// Live-op model (op-counting build only): a light sample whose contribution would be exactly +0 in every channel
+// returns black whether or not its shadow ray is blocked, so that shadow test's ops are dead. The would-be
+// contribution is evaluated here uncounted (the reference computes it only when unshadowed) and the test's ops
+// are added to g_opsShadowDead.
+static unsigned long long g_opsShadowDead = 0;
+static uint32_t fbits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, sizeof u);
+  return u;
+}
+static bool posZero3(V3 v) { return (fbits(raw(v.x)) | fbits(raw(v.y)) | fbits(raw(v.z))) == 0u; }
+#define SHADOW_TEST(ray, would_expr)                                         \
+  [&]() {                                                                    \
+    const unsigned long long t0_ = g_ops;                                    \
+    const bool sh_ = testShadow(ray);                                        \
+    const unsigned long long testOps_ = g_ops - t0_, save_ = g_ops;          \
+    const V3 would_ = (would_expr);                                          \
+    g_ops = save_;                                                           \
+    if (posZero3(would_)) g_opsShadowDead += testOps_;                       \
+    return sh_;                                                              \
+  }()
+#else
+#define SHADOW_TEST(ray, would_expr) testShadow(ray)
+#endif
 static V3 light_sample(const Intersect& ins) {
   V3 fpdf = BLACKv;
   const int index = randomInt(ins.seed, 0, C.ln);
@@ -1165,19 +1191,24 @@ static V3 light_sample(const Intersect& ins) {
     const V3 p = sampleGeometry(random2(ins.seed), aindex, normal, pdf);
     const V3 toLight = p - ins.hit;
     const V3 normToLight = normalize(toLight);
-    if (testShadow(ray_(ins.hit, toLight))) return BLACKv;
+    if (SHADOW_TEST(ray_(ins.hit, toLight),
+                    emission * fmax_(F(0.0f), dot(normal, -normToLight)) * fmax_(F(0.0f), dot(normToLight, ins.normal)) / pdf))
+      return BLACKv;
     fpdf = emission * fmax_(F(0.0f), dot(normal, -normToLight)) * fmax_(F(0.0f), dot(normToLight, ins.normal)) / pdf;
   } else if (lightCategory == POINT) {  // point.glsl:6-20
     const V3 from = readVec3(L, 1.0f, row, kLightLen), emission = readVec3(L, 4.0f, row, kLightLen);
     const V3 p = from + uniformSampleSphere(random2(ins.seed)) * F(0.1f);
     const V3 toLight = p - ins.hit;
-    if (testShadow(ray_(ins.hit, toLight))) return BLACKv;
+    if (SHADOW_TEST(ray_(ins.hit, toLight), emission * fmax_(F(0.0f), dot(normalize(toLight), ins.normal)))) return BLACKv;
     fpdf = emission * fmax_(F(0.0f), dot(normalize(toLight), ins.normal));
   } else if (lightCategory == SPOT) {  // spot.glsl:8-39
     const F ctw = readFloat(L, 1.0f, row, kLightLen), cfs = readFloat(L, 2.0f, row, kLightLen);
     const V3 from = readVec3(L, 3.0f, row, kLightLen), emission = readVec3(L, 6.0f, row, kLightLen);
     const V3 toLight = from - ins.hit;
-    if (testShadow(ray_(ins.hit, toLight))) return BLACKv;
+    if (SHADOW_TEST(ray_(ins.hit, toLight),
+                    emission * falloff(ctw, cfs, -normalize(toLight)) * fmax_(F(0.0f), dot(normalize(toLight), ins.normal)) /
+                        (length(toLight) * length(toLight))))
+      return BLACKv;
     const V3 normToLight = normalize(toLight);
     const F d = length(toLight);
     fpdf = emission * falloff(ctw, cfs, -normToLight) * fmax_(F(0.0f), dot(normalize(toLight), ins.normal)) / (d * d);
@@ -1246,7 +1277,13 @@ static void trace(Ray ray, int maxDepth, V3& e, V3& n, V3& p) {  // :16-38
     }
 #endif
     V3 wi, _fpdf;
+#ifdef SAIL_COUNT_OPS
+    const unsigned long long shadowDead = g_opsShadowDead;  // the last bounce's full shading is not live-counted
+#endif
     e = e + shade(ins, -ray.dir, wi, _fpdf) * fpdf;
+#ifdef SAIL_COUNT_OPS
+    if (last) g_opsShadowDead = shadowDead;
+#endif
     fpdf = fpdf * _fpdf;
     const F outdot = dot(ins.normal, wi);
     ray.origin = ins.hit + ins.normal * (outdot > F(kEps) ? F(0.0001f) : F(-0.0001f));
@@ -1345,12 +1382,14 @@ void oracle_reset_counters(void) {
   g_ops = 0;
   g_opsLastFull = 0;
   g_opsLastLive = 0;
+  g_opsShadowDead = 0;
 #endif
 }
-// ops of the live-op model: every op but the last bounce's dead ones (countLiveLast)
+// ops of the live-op model: every op but the last bounce's dead ones (countLiveLast) and the shadow tests of
+// light samples whose contribution would be +0 (SHADOW_TEST)
 unsigned long long oracle_ops_live(void) {
 #ifdef SAIL_COUNT_OPS
-  return g_ops - g_opsLastFull + g_opsLastLive;
+  return g_ops - g_opsLastFull + g_opsLastLive - g_opsShadowDead;
 #else
   return 0;
 #endif

@@ -1412,9 +1412,19 @@ D LightPrep lightPrep(const Ctx& c, const Hit& ins, V2 u2) {
   lp.lit = lit; lp.contrib = contrib; lp.toLight = toLight;
   return lp;
 }
+// SAIL_SHADOW_ZERO: a light sample whose unoccluded contribution is exactly +0 in every channel (the sample behind
+// the surface or the light facing away, a spot light's falloff 0) returns that +0 vector whether or not its shadow
+// ray is blocked, so the shadow sweep is skipped; any other value (-0, NaN, a nonzero channel) takes the sweep
+#ifndef SAIL_SHADOW_ZERO
+#define SAIL_SHADOW_ZERO 1
+#endif
+D bool posZero3(const V3& v) {
+  return (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
+}
 D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   const LightPrep lp = lightPrep(c, ins, u2);
   if (!lp.lit) return v3s(0.0f);
+  if (SAIL_SHADOW_ZERO && posZero3(lp.contrib)) return v3s(0.0f);
   // testShadow(Ray(hit, toLight)) (shader.light.js:24-31): unnormalised direction, no origin offset
   if (testShadow(c, mkRay(ins.hit, lp.toLight))) return v3s(0.0f);
   return lp.contrib;
@@ -1539,7 +1549,7 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
         direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
       } else if (DEFER) {  // lightSample's light prep now, its shadow test and the radiance update in the shadow pass
         const LightPrep lp = lightPrep(c, ins, u2);
-        if (lp.lit) {
+        if (lp.lit && !(SAIL_SHADOW_ZERO && posZero3(lp.contrib))) {
           sp->pending = true; sp->contrib = lp.contrib; sp->toLight = lp.toLight; sp->hit = ins.hit; sp->f = f;
           sp->emission = ins.emission; sp->fpdfOld = fpdf;
           deferE = true;

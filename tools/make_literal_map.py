@@ -113,7 +113,7 @@ MAP = {
     "specular_r_sample_f": (["material"], ["mirror"]),
     "spot_sample": (["lightPrep"], ["light_sample"]),
     "testBoundbox": (["testBoundbox"], ["testBoundbox"]),
-    "trace": (["shadeBounce"], ["trace"]),
+    "trace": (["shadeBounceT"], ["trace"]),
     "trowbridgeReitz_d": (["trD"], ["trD"]),
     "trowbridgeReitz_sample_wh": (["trSampleWh"], ["trSampleWh"]),
     "uniformSampleSphere": (["uniformSampleSphere"], ["uniformSampleSphere"]),
