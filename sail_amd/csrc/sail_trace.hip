@@ -1779,6 +1779,14 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_2BAR
 #define SAIL_SORT_2BAR 3
 #endif
+// SAIL_SHADOW_COMPACT: lit matte paths leave their shadow rays in the sort buffer (compacted, after a barrier that
+// ends the bounce's gathers) and the workgroup's first threads trace them, so waves whose lanes have no shadow ray
+// (non-matte, unlit, contribution +0) do no shadow sweep; the radiance slot holds the shadowed outcome until the
+// tracing thread writes the lit one. 1 = the pre-cull kernel, 2 = the pre-cull and room kernels, 0 = off. Measured
+// (gpurun_out/r03m, bit-identical): C4 +3.1 % (spills 74 -> 105 VGPRs), C3 -25 % (room spills 41 -> 85).
+#ifndef SAIL_SHADOW_COMPACT
+#define SAIL_SHADOW_COMPACT 1
+#endif
 // NT threads per workgroup (ungrouped kernels only; grouped ones keep 256): a 16 x NT/16 pixel block, 4096/NT
 // blocks per 64x64 tile. A larger workgroup sorts a larger pool of paths (fewer mixed waves) at the price of a
 // wider barrier.
@@ -1806,6 +1814,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if constexpr (kE4) sE4[i] = make_float4(v.x, v.y, v.z, 0.0f);
     else { sE[0][i] = v.x; sE[1][i] = v.y; sE[2][i] = v.z; }
   };
+  constexpr bool kShCompact = SAIL_SHADOW_COMPACT >= 1 && KL != 0u &&
+                              (CULL || (SAIL_SHADOW_COMPACT >= 2 && KS == SAIL_KSET_ROOM_SHAPES));
+  __shared__ int sShCnt[2];
+  int shph = 0;
   constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
                           (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
@@ -1839,6 +1851,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (CULL) __asm__ volatile("" ::: "a0");
 #endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
+  if (li < 2) sShCnt[li] = 0;
   int ph = 0;
   __syncthreads();
   // sort key: the winning primitive row when there are few enough rows (no row reads for the key, and a wave's
@@ -1986,6 +1999,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       __syncthreads();
       }
       alive = li < nAlive;
+      ShadowPending sp;
+      sp.pending = false;
+      V3 eLit = v3s(0.0f);
       int keyG = 0;  // the gathered path's sort key (packed state only)
       (void)keyG;
       PHASE_MARK(pc, 7);
@@ -2041,9 +2057,72 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
         V3 e = (deferRead && depth == 1) ? v3s(0.0f) : E_LOAD(pixel);
-        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e)))
-          shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e))) {
+          if constexpr (kShCompact) {
+            shadeBounceT<true>(c, ins, ray, S.seed + (float)depth, fpdf, e, pc, &sp);
+            if (sp.pending) {  // both outcomes of e += (emission + (0 + light * f)) * throughput, as shadeBounce
+              V3 dDark = v3s(0.0f), dLit = v3s(0.0f);
+              dDark = dDark + v3s(0.0f) * sp.f;
+              dLit = dLit + sp.contrib * sp.f;
+              eLit = e + (sp.emission + dLit) * sp.fpdfOld;
+              e = e + (sp.emission + dDark) * sp.fpdfOld;
+            }
+          } else {
+            shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+          }
+        }
         E_STORE(pixel, e);
+      }
+      if constexpr (kShCompact) {
+        if (c.ln > 0) {  // uniform
+          const bool pend = alive && sp.pending;
+          __syncthreads();  // every gather of this bounce is done: the sort buffer takes the shadow rays
+          const unsigned long long bm = __builtin_amdgcn_ballot_w64(pend);
+          if (bm != 0ull) {  // uniform over the wave
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&sShCnt[shph], __popcll(bm));
+            base = __shfl(base, 0, 64);
+            if (pend) {
+              const int d = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+              const V3 o = sp.hit, dl = sp.toLight;
+              if constexpr (kPack == 2) {
+                sSt4[0][d] = make_float4(o.x, o.y, o.z, dl.x);
+                sSt4[1][d] = make_float4(dl.y, dl.z, eLit.x, eLit.y);
+                sSt4[2][d] = make_float4(eLit.z, __int_as_float(pixel), 0.0f, 0.0f);
+              } else if constexpr (kPack == 1) {
+                sSt2[0][d] = make_float2(o.x, o.y); sSt2[1][d] = make_float2(o.z, dl.x);
+                sSt2[2][d] = make_float2(dl.y, dl.z); sSt2[3][d] = make_float2(eLit.x, eLit.y);
+                sSt2[4][d] = make_float2(eLit.z, __int_as_float(pixel));
+              } else {
+                sSt[0][d] = o.x; sSt[1][d] = o.y; sSt[2][d] = o.z; sSt[3][d] = dl.x; sSt[4][d] = dl.y;
+                sSt[5][d] = dl.z; sSt[6][d] = eLit.x; sSt[7][d] = eLit.y; sSt[8][d] = eLit.z;
+                sSt[9][d] = __int_as_float(pixel);
+              }
+            }
+          }
+          __syncthreads();
+          const int nSh = sShCnt[shph];
+          if (li == 0) sShCnt[shph ^ 1] = 0;  // the previous bounce's count: every read of it is done
+          shph ^= 1;
+          if (li < nSh) {  // testShadow(Ray(hit, toLight)) of the light sample (shader.light.js:24-31)
+            V3 o, dl, el;
+            int pix;
+            if constexpr (kPack == 2) {
+              const float4 q0 = sSt4[0][li], q1 = sSt4[1][li], q2 = sSt4[2][li];
+              o = v3(q0.x, q0.y, q0.z); dl = v3(q0.w, q1.x, q1.y); el = v3(q1.z, q1.w, q2.x);
+              pix = __float_as_int(q2.y);
+            } else if constexpr (kPack == 1) {
+              const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
+              o = v3(q0.x, q0.y, q1.x); dl = v3(q1.y, q2.x, q2.y); el = v3(q3.x, q3.y, q4.x);
+              pix = __float_as_int(q4.y);
+            } else {
+              o = v3(sSt[0][li], sSt[1][li], sSt[2][li]); dl = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
+              el = v3(sSt[6][li], sSt[7][li], sSt[8][li]); pix = __float_as_int(sSt[9][li]);
+            }
+            if (!testShadow(c, mkRay(o, dl))) E_STORE(pix, el);
+          }
+        }
       }
     }
     if (deferRead) { kPrev = k; continue; }
