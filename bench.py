@@ -395,6 +395,9 @@ def main():
                 "formula": "ops_per_segment x pixels x launch_spp x bounces / avg_launch_s / 157.3e12",
                 "kernel": ctx.kernel_name(),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                # one launch = the HIP events around the trace kernel and, with sample groups (a "_grouped" kernel),
+                # the sail_accum_kernel that adds the staged samples in order after it
+                "launch_span": "trace kernel + sail_accum_kernel" if ctx.kernel_name().endswith("_grouped") else "trace kernel",
                 "hbm": {"achieved": round(hbm_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": tiles_px * 32},
                 "valu_issue": valu_issue(pmc, avg_launch_s, local_rank),

@@ -112,7 +112,11 @@ enum sail_debug_option {
   SAIL_DEBUG_FORCE_RCCL = 5,
   /* 1: scenes on the pre-cull path are traced by the wavefront split (one sample at a time, path state in HBM, sweep /
    * shade / shadow kernels per bounce) instead of the megakernel; same results [0] */
-  SAIL_DEBUG_WAVEFRONT = 6
+  SAIL_DEBUG_WAVEFRONT = 6,
+  /* > 0: residency rounds of workgroups queued per launch when sizing the sample groups, flat kernels [36] and the
+   * pre-cull kernel [64] (SAIL_DEBUG_SAMPLE_GROUPS overrides both) */
+  SAIL_DEBUG_GROUP_ROUNDS = 7,
+  SAIL_DEBUG_CULL_GROUP_ROUNDS = 8
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 

@@ -25,6 +25,8 @@ FILTER_WAVELET, FILTER_NORMAL, FILTER_POSITION = 4, 5, 6  # need FLAG_AOV
 # sail_set_debug options (test / study switches; none changes a result)
 DEBUG_CULL_MIN_PRIMS, DEBUG_FORCE_GENERIC, DEBUG_CULL_FMA, DEBUG_SAMPLE_GROUPS, DEBUG_FORCE_RCCL = 1, 2, 3, 4, 5
 DEBUG_WAVEFRONT = 6
+DEBUG_GROUP_ROUNDS = 7
+DEBUG_CULL_GROUP_ROUNDS = 8
 # applied to every Context at creation (tests set entries with monkeypatch.setitem)
 DEBUG_DEFAULTS: dict = {}
 

@@ -131,6 +131,10 @@ struct sail_ctx {
   int shadowAnyHit = 0;
   std::vector<unsigned long long> typeMasksHost;  // staging for the per-chunk type masks (async copy source)
   int cullMinPrims = 8;  // scenes with at least this many primitives use the padded-box pre-cull
+  int lastGroups = 1;         // the last trace launch: sample groups (sail_kernel_name)
+  bool lastWavefront = false;
+  int flatGroupRounds = 36;  // sample groups: residency rounds queued per launch (flat kernels, SAIL_DEBUG_GROUP_ROUNDS)
+  int cullGroupRounds = 64;  // the same for the pre-cull kernel's 1,024-thread workgroups
   int cullFma = 1;       // SAIL_CULL_FMA=0: always the plain pre-cull form (tests)
   double primExtent = INFINITY;  // largest |padded bound| coordinate (inf: some primitive is unbounded)
   SceneBox scene{};              // union of the primitives' finite bounds (padPrimBounds)
@@ -618,11 +622,16 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       // varies with the primitives a 16x64 strip sees, so a grid of few rounds ends in a long tail (1/8 of C4: 1,020
       // workgroups = 2 rounds, 0.92 of the one-GPU rate per GPU): below 6 rounds, split the samples so that about 8
       // rounds are queued (the grouped kernel is 1,024 threads too; measured 0.95 at N = 8 with 4 groups).
+      // Round 3: more groups pay at any frame size (a shorter tail per launch); C4 at N = 1: G = 1 / 2 / 4 9.96 / 10.06
+      // / 10.12 Gseg/s (gpurun_out/r03o), so about SAIL_CULL_GROUP_ROUNDS rounds are queued.
       const double rounds = (double)owned * 4.0 / (double)(c->numCUs * 2);
-      if (rounds < 6.0) G = (int)ceil(8.0 / rounds);
+      if (rounds < (double)c->cullGroupRounds) G = (int)ceil((double)c->cullGroupRounds / rounds);
     } else {
+      // Round 3: splitting pays at full frame size too (shorter launch tails): C2 at N = 1 with G = 1 / 2 / 4 / 8 / 16
+      // 89.3 / 89.7 / 90.9 / 91.6 / 91.4 Gseg/s, C5 87.0 / 89.3 / 90.9 / 91.6 / 91.9, C3 29.2 / 28.6 / 29.2 / 29.5 / 29.4;
+      // at N = 8 (C2) G = 8 / 16 / 32 85 / 87 / 88 (gpurun_out/r03o). About 36 rounds of 7-wave residency are queued.
       const long long waves = (long long)owned * 16 * 4;
-      const long long target = (long long)c->numCUs * 4 * 7 * 4;
+      const long long target = (long long)c->numCUs * 4 * 7 * c->flatGroupRounds;
       G = (int)((target + waves - 1) / waves);
     }
     if (G > nspp) G = nspp;
@@ -667,6 +676,8 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     }
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending.emplace_back(e0, e1);
+    c->lastGroups = A.sampleGroups;
+    c->lastWavefront = wavefront;
     c->launches++;
     c->nominalSegments += (uint64_t)px * (uint64_t)nspp * (uint64_t)maxBounces;
   }
@@ -828,7 +839,9 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
   const char* k = set == SAIL_KSET_CORNELL ? "sail_trace_kernel_cornell"
                   : set == SAIL_KSET_ROOM ? "sail_trace_kernel_room"
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
-  snprintf(name, (size_t)len, "%s", k);
+  // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
+  if (c->lastWavefront) k = "sail_wf_*";
+  snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }
 
@@ -987,6 +1000,14 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
+    case SAIL_DEBUG_GROUP_ROUNDS:
+      if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
+      c->flatGroupRounds = value;
+      break;
+    case SAIL_DEBUG_CULL_GROUP_ROUNDS:
+      if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
+      c->cullGroupRounds = value;
+      break;
     default: return fail(c, SAIL_E_INVALID, "sail_set_debug: unknown option %d", option);
   }
   return SAIL_OK;

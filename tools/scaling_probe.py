@@ -3,7 +3,8 @@
 collective): predicts the strong-scaling efficiency of bench.py --gpus N before the reduce is added. A tile config
 renders the rank's tiles; a sample-split config (C5) renders its samples k = rank mod N of the whole frame.
 Usage: tools/scaling_probe.py [config] [spp] [--groups g] [--worlds 1,2,4,8]
---groups g fixes the sample-group count (SAIL_DEBUG_SAMPLE_GROUPS) instead of the host's occupancy rule."""
+--groups g fixes the sample-group count (SAIL_DEBUG_SAMPLE_GROUPS) instead of the host's occupancy rule; --rounds /
+--cull-rounds change that rule's target (SAIL_DEBUG_GROUP_ROUNDS / SAIL_DEBUG_CULL_GROUP_ROUNDS)."""
 import argparse
 import json
 import os
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--groups", type=int, default=0)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=0, help="SAIL_DEBUG_GROUP_ROUNDS (flat kernels)")
+    ap.add_argument("--cull-rounds", type=int, default=0, help="SAIL_DEBUG_CULL_GROUP_ROUNDS")
     ap.add_argument("--lib", default=None, help="a variant build of libsail_hip.so (tools/build_variants.sh)")
     a = ap.parse_args()
     if a.lib:
@@ -40,6 +43,10 @@ def main():
             ctx = capi.Context(W, H)
             if a.groups:
                 ctx.set_debug(capi.DEBUG_SAMPLE_GROUPS, a.groups)
+            if a.rounds:
+                ctx.set_debug(capi.DEBUG_GROUP_ROUNDS, a.rounds)
+            if a.cull_rounds:
+                ctx.set_debug(capi.DEBUG_CULL_GROUP_ROUNDS, a.cull_rounds)
             ctx.set_scene_dict(sc)
             ctx.set_partition(rank, world, part)
             ctx.render_schedule(inv[:32], seeds[:32], sc["eye"], B)  # warm-up
@@ -65,7 +72,7 @@ def main():
             if base is None:
                 base = rate
             print(json.dumps({"lib": os.path.basename(a.lib) if a.lib else "main", "config": a.config, "partition": "tiles" if part == capi.PART_TILES else "samples",
-                              "spp": spp, "groups": a.groups or "auto", "world": world, "rank": rank,
+                              "spp": spp, "groups": a.groups or "auto", "rounds": a.rounds or a.cull_rounds or "default", "world": world, "rank": rank,
                               "share": round(share, 5), "s": round(best, 4), "launches": int(st.launches),
                               "Gseg_per_s_per_gpu": round(rate, 3), "vs_1gpu": round(rate / base, 3),
                               "frame_speedup_if_all_ranks_like_this": round(rate / base / share, 2)}), flush=True)
