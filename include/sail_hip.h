@@ -208,7 +208,8 @@ int sail_partition_tiles(int width, int height, int rank, int world, int* out_xy
 int sail_math_probe(int fn, const float* x, const float* y, float* out, int count);
 int sail_abi_version(void);
 /* the trace kernel the context's current scene launches (a plugin-set specialisation, like the reference's
- * per-scene generated program): writes its name (e.g. "sail_trace_kernel_cornell") into name[len] */
+ * per-scene generated program): writes its name (e.g. "sail_trace_kernel_cornell") into name[len]; after a launch
+ * that split its samples into groups, the "_grouped" form it ran (followed by sail_accum_kernel) */
 int sail_kernel_name(sail_ctx* ctx, char* name, int len);
 /* device time of the last sail_filter pass (HIP events around the kernel), for the stencil's roofline */
 int sail_filter_ms(sail_ctx* ctx, double* ms);

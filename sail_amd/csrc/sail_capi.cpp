@@ -1047,6 +1047,8 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->plugins = *plugins;
+  c->lastGroups = 1;
+  c->lastWavefront = false;
   std::vector<SailPrim> prims;
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
