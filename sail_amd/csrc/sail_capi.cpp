@@ -144,7 +144,7 @@ struct sail_ctx {
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
-  float4* stage = nullptr;  // sample-group staging, allocated on first use
+  float* stage = nullptr;    // sample-group staging, allocated on first use
   size_t stageBytes = 0;
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
@@ -638,9 +638,10 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (G < 1) G = 1;
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
+    A.groupHome = SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
     A.stageStride = (long long)owned * 4096;
     if (A.sampleGroups > 1) {
-      const size_t need = (size_t)A.stageStride * (size_t)c->launchSpp * sizeof(float4);
+      const size_t need = (size_t)A.stageStride * (size_t)c->launchSpp * 3 * sizeof(float);
       if (need > c->stageBytes) {
         if (c->stage) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->stage)); c->stage = nullptr; }
         c->stageBytes = 0;

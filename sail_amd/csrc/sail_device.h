@@ -65,11 +65,13 @@ struct SailTraceArgs {
                             // 1 plain slab form, 2 fused form (host-checked scene extent, sail_capi.cpp cullFmaOk)
   int cullPrimary;          // 1: primary rays use the pre-cull too (the eye is near the scene: eyeNearScene)
   int kernelSet;            // SAIL_KSET_*: the precompiled plugin-set kernel to launch
-  // sample groups (small per-rank frames): sampleGroups workgroups share each 16x16 block, group g renders
-  // samples [g*groupSpp, (g+1)*groupSpp) into stage[k * stageStride + slot]; sail_accum_kernel then adds them
-  // to the accumulator in sample order, so the sums are bit-identical to one workgroup doing all samples
+  // sample groups: sampleGroups workgroups share each 16x16 block, group g renders samples [g*groupSpp,
+  // (g+1)*groupSpp); group 0 adds its samples to the accumulator itself, the others stage theirs, and
+  // sail_accum_kernel then adds the staged ones in sample order, so the sums are bit-identical to one workgroup
+  // doing all samples
   int sampleGroups, groupSpp;
-  float4* stage;
+  int groupHome;            // 1: group 0 accumulated its samples itself (SAIL_GROUP_HOME), the stage starts at groupSpp
+  float* stage;             // three f32 planes per sample: stage[(3k + c) * stageStride + slot]
   long long stageStride;    // slots per sample = ownedTiles * 4096
 };
 
@@ -87,6 +89,14 @@ struct SailWfState {
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a
 // set's masks may use that set's kernel; everything else runs the generic one.
 enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
+// SAIL_GROUP_HOME: with sample groups, the room kernel's first group adds its samples to the accumulator itself and
+// the other groups stage theirs (C3 +1 %); in the other kernels the extra path costs more registers than the staged
+// samples it saves (C2 -1.4 %, C4 -0.6 %), so every group stages. 0 = every kernel stages. Shared by the kernel and
+// the host (which tells sail_accum_kernel where the staged samples start).
+#ifndef SAIL_GROUP_HOME
+#define SAIL_GROUP_HOME 1
+#endif
+#define SAIL_GROUP_HOME_FOR(kernelSet) (SAIL_GROUP_HOME && (kernelSet) == SAIL_KSET_ROOM)
 // the exact segment counter is kept as this many partial sums (spread atomics), added on readback
 #define SAIL_SEG_SLOTS 64
 #define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))

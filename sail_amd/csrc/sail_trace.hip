@@ -1615,7 +1615,9 @@ D TileWork tileWork(const SailTraceArgs& A) {
   w.ownedTile = w.bid / kPer; w.sub = w.bid % kPer;
   return w;
 }
-// The staged radiance of sample k at lane li of block bid: stage row k, in the 256-thread (16 x 16 block) slot order
+// The staged radiance of sample k at lane li of block bid (groups after the first; the first group, which holds
+// the launch's first samples, adds its own to the accumulator directly): stage planes 3k..3k+2, in the 256-thread
+// (16 x 16 block) slot order
 // sail_accum_kernel reads -- slot (ownedTile * 16 + block16) * 256 + (y mod 16) * 16 + (x mod 16) -- whatever NT is
 template <int NT = 256>
 D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
@@ -1628,7 +1630,11 @@ D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
     const int ly = (sub >> 2) * (NT / 16) + (li >> 4), lx = (sub & 3) * 16 + (li & 15);
     slot = ((size_t)ownedTile * 16 + (size_t)((ly >> 4) * 4 + (lx >> 4))) * 256 + (size_t)((ly & 15) * 16 + (lx & 15));
   }
-  A.stage[(size_t)k * (size_t)A.stageStride + slot] = make_float4(e.x, e.y, e.z, 0.0f);
+  // three planes per sample (12 B per pixel instead of a float4's 16)
+  float* const st = A.stage + (size_t)k * 3u * (size_t)A.stageStride + slot;
+  st[0] = e.x;
+  st[A.stageStride] = e.y;
+  st[2 * A.stageStride] = e.z;
 }
 
 }  // namespace
@@ -1684,7 +1690,8 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   __shared__ float4 sAcc[256];
   __shared__ float2 sST[256];
   const int li = threadIdx.x;
-  sAcc[li] = grouped ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : A.accum[pix];
+  const bool home = !grouped;  // the generic kernel's groups all stage (SAIL_GROUP_HOME_FOR)
+  sAcc[li] = home ? A.accum[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   sST[li] = make_float2(((float)x + 0.5f) / (float)A.W, ((float)y + 0.5f) / (float)A.H);
   const bool aovGroup = tw.kEnd == A.spp;  // the group holding the launch's last sample writes the AOVs
   const bool wantAov = (A.aovN || A.aovP) && aovGroup;
@@ -1704,10 +1711,10 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
     const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
     const long long aovPix = (wantAov && k == A.spp - 1) ? (long long)pix : -1;
     const V3 e = trace(c, ray, S.seed, A.maxBounces, A.aovN, A.aovP, aovPix, segs, pc);
-    if (grouped) stageSample(A, k, tw.bid, threadIdx.x, e);
+    if (!home) stageSample(A, k, tw.bid, threadIdx.x, e);
     else { float4 acc = sAcc[li]; accumulateSample(acc, e, S, A.accumMode); sAcc[li] = acc; }
   }
-  if (!grouped) A.accum[pix] = sAcc[li];
+  if (home) A.accum[pix] = sAcc[li];
 #if SAIL_PHASE_TIMING
   PHASE_MARK(pc, 7);  // accumulate + store
   if (lane == 0)
@@ -1861,7 +1868,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   const bool byPrim = SAIL_SORT_BY_PRIM && A.n < kKeys;
   const size_t pixG = (size_t)y * A.W + x;
   constexpr bool grouped = GROUPED;
-  float4 acc = (valid && !grouped) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  // the room kernel's first group accumulates its samples itself (SAIL_GROUP_HOME_FOR, sail_device.h)
+  constexpr bool kHome = SAIL_GROUP_HOME && KS == SAIL_KSET_ROOM_SHAPES && !CULL;
+  const bool home = !grouped || (kHome && tw.kBeg == 0);
+  float4 acc = (valid && home) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
@@ -1878,7 +1888,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   auto settlePrev = [&](bool alive) {
     if (valid && kPrev >= 0) {
       const V3 er = E_LOAD(li);
-      if (grouped) stageSample<NT>(A, kPrev, tw.bid, li, er);
+      if (!home) stageSample<NT>(A, kPrev, tw.bid, li, er);
       else accumulateSample(acc, er, constRow<SailSample>(A.samples, kPrev), A.accumMode);
     }
     if (!alive) E_STORE(li, v3s(0.0f));
@@ -2129,7 +2139,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     __syncthreads();
     if (valid) {
       const V3 er = E_LOAD(li);
-      if (grouped) stageSample<NT>(A, k, tw.bid, li, er);
+      if (!home) stageSample<NT>(A, k, tw.bid, li, er);
       else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
@@ -2138,7 +2148,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     __syncthreads();
     settlePrev(true);
   }
-  if (valid && !grouped) A.accum[pixG] = acc;
+  if (valid && home) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
   if (lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
@@ -2390,11 +2400,12 @@ extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArg
   const int x = tx * 64 + (sub & 3) * 16 + (li & 15), y = ty * 64 + (sub >> 2) * 16 + (li >> 4);
   if (x >= A.W || y >= A.H) return;
   const size_t pix = (size_t)y * A.W + x;
-  float4 acc = A.accum[pix];
-  const float4* st = A.stage + (long long)bid * 256 + li;
-  for (int k = 0; k < A.spp; k++) {
-    const float4 v = st[(size_t)k * A.stageStride];
-    accumulateSample(acc, v3(v.x, v.y, v.z), constRow<SailSample>(A.samples, k), A.accumMode);
+  float4 acc = A.accum[pix];  // holds the first group's samples already (SAIL_GROUP_HOME)
+  const float* st = A.stage + (long long)bid * 256 + li;
+  for (int k = A.groupHome ? A.groupSpp : 0; k < A.spp; k++) {
+    const float* q = st + (size_t)k * 3u * (size_t)A.stageStride;
+    accumulateSample(acc, v3(q[0], q[A.stageStride], q[2 * A.stageStride]), constRow<SailSample>(A.samples, k),
+                     A.accumMode);
   }
   A.accum[pix] = acc;
 }
