@@ -104,10 +104,18 @@ enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
 #define SAIL_KSET_CORNELL_TEX 0u
 #define SAIL_KSET_CORNELL_LIGHTS 0u
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, the UI demo): no quadrics or disks
+#ifndef SAIL_KSET_ROOM_SHAPES
 #define SAIL_KSET_ROOM_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_RECTANGLE) | (1u << SAIL_CORNELLBOX))
+#endif
+#ifndef SAIL_KSET_ROOM_MATS
 #define SAIL_KSET_ROOM_MATS 0xffffffffu
+#endif
+#ifndef SAIL_KSET_ROOM_TEX
 #define SAIL_KSET_ROOM_TEX 0xffffffffu
+#endif
+#ifndef SAIL_KSET_ROOM_LIGHTS
 #define SAIL_KSET_ROOM_LIGHTS 0xffffffffu
+#endif
 
 struct SailFilterArgs {
   const float4* accum;

@@ -1750,6 +1750,9 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_PRIO_MIXED
 #define SAIL_PRIO_MIXED 2
 #endif
+#ifndef SAIL_PRIO_MATTE
+#define SAIL_PRIO_MATTE 0
+#endif
 // SAIL_STATE_PACK (SAIL_STATE_PACK_CULL for the pre-cull kernel): the migrated path state as 15 floats (0), six float2
 // (1, ds_*_b64) or three float4 (2, ds_*_b128), the local hit point recomputed when packed; SAIL_E4 (_CULL): each
 // pixel's radiance slot as one float4. Measured with priority 2 (gpurun_out/r03g, Gseg/s C1 / C3 / C4): pack 1
@@ -2047,18 +2050,28 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
         }
         ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
+        bool mixedW = false;
+        (void)mixedW;
 #if SAIL_PRIO_MIXED
         {  // a wave whose live paths have different sort keys runs several hit-record / material branches: raise its
            // issue priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
           const int kk = kPack ? keyG : sw.bi;
           const int k0 = __builtin_amdgcn_readfirstlane(kk);
-          if (__builtin_amdgcn_ballot_w64(kk != k0) != 0ull) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
+          mixedW = __builtin_amdgcn_ballot_w64(kk != k0) != 0ull;
+          if (mixedW) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
           else __builtin_amdgcn_s_setprio(0);
         }
 #endif
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
         const Hit ins = hitRecordU<kPack != 0>(c, ray, sw);
+#if SAIL_PRIO_MATTE
+        // study: a uniform wave of lit matte paths (light sample + shadow sweep ahead, the longest bounce) at
+        // priority SAIL_PRIO_MATTE
+        if (KL != 0u && !mixedW &&
+            __builtin_amdgcn_ballot_w64(isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) != 0ull)
+          __builtin_amdgcn_s_setprio(SAIL_PRIO_MATTE);
+#endif
         PHASE_MARK(pc, 1);
         if (depth == 1 && aovSample) {
           const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
