@@ -64,6 +64,8 @@ def main():
             "salu_insts_per_wave": c.get("SQ_INSTS_SALU", 0) / waves,
             # beyond the one float4 accumulator store per lane: scratch (register spill) stores
             "vmem_writes_per_wave": c.get("SQ_INSTS_VMEM_WR", 0) / waves,
+            # per segment-lane as well: a grouped launch has more, shorter waves (fewer samples each)
+            "vmem_writes_per_segment_lane": c.get("SQ_INSTS_VMEM_WR", 0) * 64 / segs,
             "vmem_reads_per_segment_lane": c.get("SQ_INSTS_VMEM_RD", 0) * 64 / segs,
         }
         sq = passes.get("sq")
