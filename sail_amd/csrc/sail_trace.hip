@@ -182,6 +182,7 @@ struct Hit {
 };
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
+  const SailPrim* cprims;  // rows for the candidate loops' per-lane reads: an LDS copy when it fits (SAIL_CULL_LDS_ROWS)
   const unsigned long long* typeMasks;
   int n, tn, ln;
   uint32_t matMask, texMask, lightMask;
@@ -888,7 +889,7 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
     const bool has = m != 0ull;
     const int i = base + __builtin_ctzll(has ? m : tm);
     m &= m - 1ull;  // 0 stays 0
-    const SailPrim& p = PRIM(c, i);
+    const SailPrim& p = c.cprims[i];
     V3 hl = v3s(0.0f);
     const float t = typedT<T>(p, r, &hl);
     const bool take = has & ((t < best) | ((t == best) & (i < bi)));
@@ -902,7 +903,7 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
     if (m != 0ull) {
       const int i = base + __builtin_ctzll(m);
       m &= m - 1ull;
-      const SailPrim& p = PRIM(c, i);
+      const SailPrim& p = c.cprims[i];
 #if SAIL_CAND_RECULL
       if (!padHit(p, r, best)) continue;
 #endif
@@ -1673,6 +1674,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.prims = sPrims;
 #else
   c.prims = A.prims;
+  c.cprims = A.prims;
 #endif
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
@@ -1789,6 +1791,11 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SORT_2BAR
 #define SAIL_SORT_2BAR 3
 #endif
+// SAIL_CULL_LDS_ROWS: scenes of at most this many rows are copied into LDS by each pre-cull workgroup, and the
+// candidate loops read their per-lane rows from there instead of global memory (0 = off)
+#ifndef SAIL_CULL_LDS_ROWS
+#define SAIL_CULL_LDS_ROWS 96
+#endif
 // SAIL_SHADOW_COMPACT: lit matte paths leave their shadow rays in the sort buffer (compacted, after a barrier that
 // ends the bounce's gathers) and the workgroup's first threads trace them, so waves whose lanes have no shadow ray
 // (non-matte, unlit, contribution +0) do no shadow sweep; the radiance slot holds the shadowed outcome until the
@@ -1846,6 +1853,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   Ctx c;
   c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
   c.prims = A.prims;
+  c.cprims = A.prims;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
@@ -1862,6 +1870,17 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
   if (li < 2) sShCnt[li] = 0;
+  // the pre-cull kernel's candidate loops read rows per lane: from an LDS copy of the scene when it fits
+  constexpr int kLdsRows = CULL ? SAIL_CULL_LDS_ROWS : 0;
+  __shared__ float4 sPrimL[kLdsRows > 0 ? kLdsRows * (int)(sizeof(SailPrim) / 16) : 1];
+  if constexpr (kLdsRows > 0) {
+    if (A.n <= kLdsRows) {  // uniform
+      const float4* src = reinterpret_cast<const float4*>(A.prims);
+      const int nv = A.n * (int)(sizeof(SailPrim) / 16);
+      for (int i = li; i < nv; i += NT) sPrimL[i] = src[i];
+      c.cprims = reinterpret_cast<const SailPrim*>(sPrimL);
+    }
+  }
   int ph = 0;
   __syncthreads();
   // sort key: the winning primitive row when there are few enough rows (no row reads for the key, and a wave's
@@ -2269,6 +2288,7 @@ D Ctx wfCtx(const SailTraceArgs& A) {
   Ctx c;
   c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
   c.prims = A.prims;
+  c.cprims = A.prims;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
