@@ -34,6 +34,18 @@ using namespace sm;
 #ifndef SAIL_SS_UNIT
 #define SAIL_SS_UNIT 1
 #endif
+// SAIL_CULL_LDS_HIT: the pre-cull kernel's hit record reads its winner's row from the LDS copy of the rows (SAIL_CULL_LDS_ROWS);
+// SAIL_CULL_LDS_TP = r: texParams tables of at most r rows are copied into LDS as well (0 = off)
+#ifndef SAIL_CULL_LDS_HIT
+#define SAIL_CULL_LDS_HIT 1
+#endif
+#ifndef SAIL_CULL_LDS_TP
+#define SAIL_CULL_LDS_TP 136
+#endif
+// SAIL_CULL_LDS_LIGHTS = r: light tables of at most r rows are copied into LDS too (0 = off)
+#ifndef SAIL_CULL_LDS_LIGHTS
+#define SAIL_CULL_LDS_LIGHTS 0
+#endif
 #ifndef SAIL_PRIMS_LDS
 #define SAIL_PRIMS_LDS 0
 #endif
@@ -183,6 +195,7 @@ struct Hit {
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
   const SailPrim* cprims;  // rows for the candidate loops' per-lane reads: an LDS copy when it fits (SAIL_CULL_LDS_ROWS)
+  const float* tpl;        // pre-cull kernel: texParams rows, an LDS copy when they fit (SAIL_CULL_LDS_TP)
   const unsigned long long* typeMasks;
   int n, tn, ln;
   uint32_t matMask, texMask, lightMask;
@@ -210,7 +223,10 @@ template <typename T> D const T& constRow(const T* base, int i) { return *(const
 #endif
 
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
-D float TP(const Ctx& c, int row, int col) { return constRow<float>(c.tp, row * 16 + col); }
+D float TP(const Ctx& c, int row, int col) {
+  if (SAIL_CULL_LDS_TP && c.cullPrims) return c.tpl[row * 16 + col];  // the pre-cull kernel (compile-time)
+  return constRow<float>(c.tp, row * 16 + col);
+}
 D V3 TP3(const Ctx& c, int row, int col) { return v3(TP(c, row, col), TP(c, row, col + 1), TP(c, row, col + 2)); }
 
 // the square root of the warps and BSDF terms whose argument is in [0, 1] by construction (sail_math.h sqrt01)
@@ -1019,7 +1035,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // precondition: bi >= 0 is a sweep winner, so its shape is compiled into this kernel (primT returns
   // MAX_DISTANCE for any other row, which never wins): no zero record is needed on any path -- a divergent
   // zero default would be materialised for every lane before the dispatch
-  const SailPrim& p = PRIM(c, bi);
+  const SailPrim& p = (SAIL_CULL_LDS_HIT && c.cullPrims) ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
   switch (p.type) {
     case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
@@ -1081,7 +1097,7 @@ D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc)
 D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
   normal = v3s(0.0f);
   pdf = 0.0f;
-  const SailPrim& p = PRIM(c, row);
+  const SailPrim& p = (SAIL_CULL_LDS_HIT && c.cullPrims) ? c.cprims[row] : PRIM(c, row);
   const float s = sgn(p.rev);
   switch (p.type) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
@@ -1675,6 +1691,7 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #else
   c.prims = A.prims;
   c.cprims = A.prims;
+  c.tpl = A.texparams;
 #endif
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
@@ -1792,9 +1809,12 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #define SAIL_SORT_2BAR 3
 #endif
 // SAIL_CULL_LDS_ROWS: scenes of at most this many rows are copied into LDS by each pre-cull workgroup, and the
-// candidate loops read their per-lane rows from there instead of global memory (0 = off)
+// candidate loops read their per-lane rows from there instead of global memory (0 = off). C4 +4.3 %; with the hit
+// record's and light sampler's rows and the texParams table there too (SAIL_CULL_LDS_HIT / _TP) +8.8 %
+// (gpurun_out/r03aa, r03ab). 72 rows + 136 texParams rows keep the block at 79.9 KB: two 1,024-thread workgroups
+// per CU.
 #ifndef SAIL_CULL_LDS_ROWS
-#define SAIL_CULL_LDS_ROWS 96
+#define SAIL_CULL_LDS_ROWS 72
 #endif
 // SAIL_SHADOW_COMPACT: lit matte paths leave their shadow rays in the sort buffer (compacted, after a barrier that
 // ends the bounce's gathers) and the workgroup's first threads trace them, so waves whose lanes have no shadow ray
@@ -1854,6 +1874,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
   c.prims = A.prims;
   c.cprims = A.prims;
+  c.tpl = A.texparams;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
@@ -1879,6 +1900,23 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       const int nv = A.n * (int)(sizeof(SailPrim) / 16);
       for (int i = li; i < nv; i += NT) sPrimL[i] = src[i];
       c.cprims = reinterpret_cast<const SailPrim*>(sPrimL);
+    }
+  }
+  constexpr int kLdsLights = CULL ? SAIL_CULL_LDS_LIGHTS : 0;  // light rows (18 floats) read per lane
+  __shared__ float sLtL[kLdsLights > 0 ? kLdsLights * 18 : 1];
+  if constexpr (kLdsLights > 0) {
+    if (A.ln <= kLdsLights) {  // uniform
+      for (int i = li; i < A.ln * 18; i += NT) sLtL[i] = A.lights[i];
+      c.lt = sLtL;
+    }
+  }
+  constexpr int kLdsTp = CULL ? SAIL_CULL_LDS_TP : 0;
+  __shared__ float4 sTpL[kLdsTp > 0 ? kLdsTp * 4 : 1];
+  if constexpr (kLdsTp > 0) {
+    if (A.tn <= kLdsTp) {  // uniform
+      const float4* src = reinterpret_cast<const float4*>(A.texparams);
+      for (int i = li; i < A.tn * 4; i += NT) sTpL[i] = src[i];
+      c.tpl = reinterpret_cast<const float*>(sTpL);
     }
   }
   int ph = 0;
@@ -2289,6 +2327,7 @@ D Ctx wfCtx(const SailTraceArgs& A) {
   c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
   c.prims = A.prims;
   c.cprims = A.prims;
+  c.tpl = A.texparams;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
