@@ -42,6 +42,14 @@ using namespace sm;
 #ifndef SAIL_CULL_LDS_TP
 #define SAIL_CULL_LDS_TP 136
 #endif
+// SAIL_FLAT_LDS = r: the flat compacting kernels copy scenes of at most r rows (and SAIL_FLAT_LDS_TP texParams rows)
+// into LDS for their per-lane hit-record, light-sampler and texParams reads (0 = off; study switch)
+#ifndef SAIL_FLAT_LDS
+#define SAIL_FLAT_LDS 0
+#endif
+#ifndef SAIL_FLAT_LDS_TP
+#define SAIL_FLAT_LDS_TP 16
+#endif
 // SAIL_CULL_LDS_LIGHTS = r: light tables of at most r rows are copied into LDS too (0 = off)
 #ifndef SAIL_CULL_LDS_LIGHTS
 #define SAIL_CULL_LDS_LIGHTS 0
@@ -195,7 +203,8 @@ struct Hit {
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
   const SailPrim* cprims;  // rows for the candidate loops' per-lane reads: an LDS copy when it fits (SAIL_CULL_LDS_ROWS)
-  const float* tpl;        // pre-cull kernel: texParams rows, an LDS copy when they fit (SAIL_CULL_LDS_TP)
+  const float* tpl;        // texParams rows, an LDS copy when they fit (SAIL_CULL_LDS_TP, SAIL_FLAT_LDS)
+  bool rowCopy, tpCopy;    // per-lane hit-record / light-sampler row reads and texParams reads go through cprims / tpl
   const unsigned long long* typeMasks;
   int n, tn, ln;
   uint32_t matMask, texMask, lightMask;
@@ -224,7 +233,7 @@ template <typename T> D const T& constRow(const T* base, int i) { return *(const
 
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
 D float TP(const Ctx& c, int row, int col) {
-  if (SAIL_CULL_LDS_TP && c.cullPrims) return c.tpl[row * 16 + col];  // the pre-cull kernel (compile-time)
+  if (c.tpCopy) return c.tpl[row * 16 + col];  // kernels with table copies in LDS (compile-time)
   return constRow<float>(c.tp, row * 16 + col);
 }
 D V3 TP3(const Ctx& c, int row, int col) { return v3(TP(c, row, col), TP(c, row, col + 1), TP(c, row, col + 2)); }
@@ -1035,7 +1044,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // precondition: bi >= 0 is a sweep winner, so its shape is compiled into this kernel (primT returns
   // MAX_DISTANCE for any other row, which never wins): no zero record is needed on any path -- a divergent
   // zero default would be materialised for every lane before the dispatch
-  const SailPrim& p = (SAIL_CULL_LDS_HIT && c.cullPrims) ? c.cprims[bi] : PRIM(c, bi);
+  const SailPrim& p = c.rowCopy ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
   switch (p.type) {
     case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
@@ -1097,7 +1106,7 @@ D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc)
 D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
   normal = v3s(0.0f);
   pdf = 0.0f;
-  const SailPrim& p = (SAIL_CULL_LDS_HIT && c.cullPrims) ? c.cprims[row] : PRIM(c, row);
+  const SailPrim& p = c.rowCopy ? c.cprims[row] : PRIM(c, row);
   const float s = sgn(p.rev);
   switch (p.type) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
@@ -1692,6 +1701,8 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
   c.prims = A.prims;
   c.cprims = A.prims;
   c.tpl = A.texparams;
+  c.rowCopy = false;
+  c.tpCopy = false;
 #endif
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
@@ -1875,6 +1886,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.prims = A.prims;
   c.cprims = A.prims;
   c.tpl = A.texparams;
+  c.rowCopy = false;
+  c.tpCopy = false;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
@@ -1891,8 +1904,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
   if (li < 2) sShCnt[li] = 0;
-  // the pre-cull kernel's candidate loops read rows per lane: from an LDS copy of the scene when it fits
-  constexpr int kLdsRows = CULL ? SAIL_CULL_LDS_ROWS : 0;
+  // the pre-cull kernel's candidate loops read rows per lane: from an LDS copy of the scene when it fits (and the
+  // flat kernels' per-lane hit-record, light-sampler and texParams reads with SAIL_FLAT_LDS)
+  constexpr int kLdsRows = CULL ? SAIL_CULL_LDS_ROWS : SAIL_FLAT_LDS;
+  c.rowCopy = CULL ? (SAIL_CULL_LDS_HIT != 0) : (SAIL_FLAT_LDS != 0);
   __shared__ float4 sPrimL[kLdsRows > 0 ? kLdsRows * (int)(sizeof(SailPrim) / 16) : 1];
   if constexpr (kLdsRows > 0) {
     if (A.n <= kLdsRows) {  // uniform
@@ -1910,7 +1925,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       c.lt = sLtL;
     }
   }
-  constexpr int kLdsTp = CULL ? SAIL_CULL_LDS_TP : 0;
+  constexpr int kLdsTp = CULL ? SAIL_CULL_LDS_TP : (SAIL_FLAT_LDS ? SAIL_FLAT_LDS_TP : 0);
+  c.tpCopy = kLdsTp > 0;
   __shared__ float4 sTpL[kLdsTp > 0 ? kLdsTp * 4 : 1];
   if constexpr (kLdsTp > 0) {
     if (A.tn <= kLdsTp) {  // uniform
@@ -2328,6 +2344,8 @@ D Ctx wfCtx(const SailTraceArgs& A) {
   c.prims = A.prims;
   c.cprims = A.prims;
   c.tpl = A.texparams;
+  c.rowCopy = false;
+  c.tpCopy = false;
   c.n = A.n; c.tn = A.tn; c.ln = A.ln;
   c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
   c.fcx = 0.0f; c.fcy = 0.0f;
