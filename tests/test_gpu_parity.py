@@ -338,6 +338,23 @@ def test_candidate_sweep_chunks_and_ties(gpu, fixtures, monkeypatch, cull):
     assert st.segments == segs
 
 
+@pytest.mark.parametrize("extra_rows,extra_tp", [(0, 0), (6, 0), (0, 3), (6, 3)])
+def test_precull_lds_table_limits(gpu, fixtures, extra_rows, extra_tp):
+    """the pre-cull kernel's LDS copies hold scenes of up to 72 rows and texParams tables of up to 136 rows; past
+    either limit that table is read from global memory: C4 (67 rows, 134 texParams rows) grown across each limit"""
+    sc = dict(fixtures["scenes"]["C4"])
+    assert sc["n"] + 6 > 72 and sc["tn"] + 3 > 136 and sc["n"] <= 72 and sc["tn"] <= 136
+    objs, tp = list(sc["objects"]), list(sc["texparams"])
+    sc["objects"] = objs + objs[18:18 * (1 + extra_rows)]       # duplicates of rows 1.. (ties: the lower row wins)
+    sc["n"] = sc["n"] + extra_rows
+    sc["texparams"] = tp + tp[:16 * extra_tp]
+    sc["tn"] = sc["tn"] + extra_tp
+    got, want, st, segs, gaov, waov = _render_both({"scenes": {"C4L": sc}}, "C4L", 40, 32, 2, 6, aov=True, launch=2)
+    assert bit_equal(got, want).all()
+    assert bit_equal(gaov[0], waov[0]).all() and bit_equal(gaov[1], waov[1]).all()
+    assert st.segments == segs
+
+
 # ---- plugin-set kernels: the Cornell-box kernel (C1 scenes by default) and the generic one agree bit for bit --
 @pytest.mark.parametrize("force", ["0", "1"])
 def test_plugin_set_kernels(gpu, fixtures, monkeypatch, force):
