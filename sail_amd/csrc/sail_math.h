@@ -185,7 +185,6 @@ SM_D float clamp_(float x, float lo, float hi) {
   return fmin_(fmax_(x, lo), hi);
 }
 SM_D float fract_(float x) { return x - floorf(x); }
-SM_D float sqrtf_(float x) { return __builtin_sqrtf(x); }
 // sqrtf_ for arguments that are +-0, NaN or in [2^-96, 1] by construction, where v_sqrt_f32 plus the
 // two-neighbour residual correction equals the IEEE square root bit for bit (tools/sqrt01_probe.hip: every such f32
 // on an MI355X; below 2^-96 the hardware root needs the general lowering's scaling). The callers' arguments:
@@ -203,6 +202,27 @@ SM_D float sqrt01(float x) {
   if (__builtin_fmaf(-sup, s, x) > 0.0f) r = sup;
   return r;
 }
+// The general square root by the same core: the residual correction is exact wherever v_sqrt_f32 needs no
+// scaling -- +-0, NaN, +inf and every f32 >= 2^-96 (tools/sqrt01_probe.hip checks all of them against the IEEE
+// lowering) -- and the rest (tiny positives, subnormals, negatives) takes the compiler's IEEE sqrt behind a real
+// branch (an empty volatile asm keeps it from being if-converted into every call). Exact on all 2^32 inputs
+// (profiles/r03_sqrt_probe.json) but measured C2 +0.1 %, C3 -0.5 %, C4 -0.6 %, so SAIL_SQRT_CORE defaults to 0 (IEEE).
+#ifndef SAIL_SQRT_CORE
+#define SAIL_SQRT_CORE 0
+#endif
+SM_D float sqrtg(float x) {
+#if SAIL_SQRT_CORE
+  if (__builtin_expect(x < 0x1p-96f && x != 0.0f, 0)) {
+    float xx = x;
+    __asm__ volatile("" : "+v"(xx));
+    return __builtin_sqrtf(xx);
+  }
+  return sqrt01(x);
+#else
+  return __builtin_sqrtf(x);
+#endif
+}
+SM_D float sqrtf_(float x) { return sqrtg(x); }
 // GLSL division a / b := a * RN(1/b) (the reciprocal-multiply form shader compilers emit, with the reciprocal
 // correctly rounded; oracle/ref_math.h div_s). RN(1/b) = one Newton step from the hardware reciprocal, equal to
 // the IEEE 1.0f / b for every f32 b with 2^-126 <= |b| <= 2^126 (all 2^32 inputs checked on an MI355X:
