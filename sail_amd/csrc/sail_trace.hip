@@ -1835,6 +1835,9 @@ __device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
 #ifndef SAIL_SHADOW_COMPACT
 #define SAIL_SHADOW_COMPACT 1
 #endif
+#ifndef SAIL_PROBE_MAJORITY
+#define SAIL_PROBE_MAJORITY 0
+#endif
 // NT threads per workgroup (ungrouped kernels only; grouped ones keep 256): a 16 x NT/16 pixel block, 4096/NT
 // blocks per 64x64 tile. A larger workgroup sorts a larger pool of paths (fewer mixed waves) at the price of a
 // wider barrier.
@@ -2137,6 +2140,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 #endif
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
+#if SAIL_PROBE_MAJORITY
+        // timing probe only (not bit-exact): lanes whose key differs from lane 32's skip this bounce's shading
+        const int kMid = __builtin_amdgcn_readlane(kPack ? keyG : sw.bi, 32);
+        const unsigned long long midM = __builtin_amdgcn_ballot_w64((kPack ? keyG : sw.bi) == kMid);
+        if ((kPack ? keyG : sw.bi) == kMid || midM == 0ull) {
+#endif
         const Hit ins = hitRecordU<kPack != 0>(c, ray, sw);
 #if SAIL_PRIO_MATTE
         // study: a uniform wave of lit matte paths (light sample + shadow sweep ahead, the longest bounce) at
@@ -2168,6 +2177,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           }
         }
         E_STORE(pixel, e);
+#if SAIL_PROBE_MAJORITY
+        }
+#endif
       }
       if constexpr (kShCompact) {
         if (c.ln > 0) {  // uniform
@@ -2285,9 +2297,13 @@ SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, SAIL_GENERIC_TILE, f
 #ifndef SAIL_CORNELL_NT
 #define SAIL_CORNELL_NT 256
 #endif
+// threads per workgroup of the grouped flat kernels (the sort pool of a sample group's workgroup)
+#ifndef SAIL_CORNELL_GROUP_NT
+#define SAIL_CORNELL_GROUP_NT 256
+#endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
                       SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS,
-                      SAIL_CORNELL_NT, 256)
+                      SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT)
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
 #ifndef SAIL_TRACE_ROOM_MIN_WAVES
 #define SAIL_TRACE_ROOM_MIN_WAVES 7
@@ -2301,8 +2317,12 @@ SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, S
 #ifndef SAIL_ROOM_NT
 #define SAIL_ROOM_NT 256
 #endif
+#ifndef SAIL_ROOM_GROUP_NT
+#define SAIL_ROOM_GROUP_NT 256
+#endif
 SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
-                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, 256)
+                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT,
+                      SAIL_ROOM_GROUP_NT)
 // the pre-cull kernel serves scenes with many primitives (C4: 7 waves measured best of 5-8)
 #ifndef SAIL_TRACE_CULL_MIN_WAVES
 #define SAIL_TRACE_CULL_MIN_WAVES 8
@@ -2757,8 +2777,8 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
     if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks * 256 / (gnt)), dim3(gnt), 0, s, A);     \
     else hipLaunchKernelGGL(k, dim3(blocks * 256 / (nt)), dim3(nt), 0, s, A);                     \
   } while (0)
-  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT, 256);
-  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT, 256);
+  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT);
+  else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT);
   else if (A.cullPrims) SAIL_LAUNCH_NT(sail_trace_kernel_cull, SAIL_CULL_NT, SAIL_CULL_GROUP_NT);
   else SAIL_LAUNCH(sail_trace_kernel);
 #undef SAIL_LAUNCH
