@@ -446,6 +446,41 @@ D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
 #endif
 }
 
+// SAIL_BOX_UNIFIED: one hit record for both axis-aligned box shapes (a wave holding Cube and Cornellbox lanes, e.g. the
+// README box's ceiling light next to its walls, runs one face chain instead of two). The face chains test the same
+// conditions; the Cube's normal is sgn(rev) * n and the Cornellbox's is -n == -1 * n bit for bit (zeros included);
+// only the surface colour differs (texture vs wall chain).
+// Measured (bit-identical, profiles/r03_variants_box_unified.jsonl): C2 -0.8 %, C3 +0.7 %, C4 +0.1 %; so 2 (default) =
+// the room kernel only, 1 = every kernel, 0 = off.
+#ifndef SAIL_BOX_UNIFIED
+#define SAIL_BOX_UNIFIED 2
+#endif
+#define SAIL_BOX_UNIFIED_ON(ks) (SAIL_BOX_UNIFIED == 1 || (SAIL_BOX_UNIFIED == 2 && (ks) == SAIL_KSET_ROOM_SHAPES))
+D void boxHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h, bool cornell) {
+  h.hit = r.o + t * r.d;
+  const float s = cornell ? -1.0f : sgn(p.rev);
+  h.normal = s * normalForCornellbox(r.o + t * r.d, p);
+  dpdBox(h.normal, h.dpdu, h.dpdv);
+  const V3 mn = P3(p, 0), mx = P3(p, 3), x = h.hit;
+  if (cornell) {
+    if (x.x < mn.x + 0.0001f) h.sc = v3(0.25f, 0.75f, 0.25f);
+    else if (x.x > mx.x - 0.0001f) h.sc = v3(0.25f, 0.25f, 0.75f);
+    else if (x.y < mn.y + 0.0001f) h.sc = v3s(1.0f);
+    else if (x.y > mx.y - 0.0001f) h.sc = v3s(1.0f);
+    else if (x.z > mn.z + 0.0001f) h.sc = v3s(1.0f);
+    else h.sc = v3s(0.0f);
+  } else {
+    V2 uv = v2(0.0f, 0.0f);
+    if (needsUV(p)) {
+      const V3 tr = mx - mn, hh = h.hit - mn;  // getCubeUV cube.glsl:54-63
+      if (hh.x < mn.x + 0.0001f || hh.x > mx.x - 0.0001f) uv = v2(fdiv(hh.y, tr.y), fdiv(hh.z, tr.z));
+      else if (hh.y < mn.y + 0.0001f || hh.y > mx.y - 0.0001f) uv = v2(fdiv(hh.x, tr.x), fdiv(hh.z, tr.z));
+      else uv = v2(fdiv(hh.x, tr.x), fdiv(hh.y, tr.y));
+    }
+    h.sc = getSurfaceColor(c, uv, p);
+  }
+}
+
 // The quadrics' bounding-box test (testBoundboxFor*) and their root search are both pure predicates on the
 // ray, so their order is free: the discriminant rejects most rays more cheaply than the six-divide slab test,
 // and only candidate hits pay the exact slab test (same results; C3 +4 %, C4 +5 %, measured).
@@ -1046,8 +1081,13 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // zero default would be materialised for every lane before the dispatch
   const SailPrim& p = c.rowCopy ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
+  const bool boxU = SAIL_BOX_UNIFIED_ON(c.kShapes);  // a compile-time constant in each kernel
+  if (boxU && ((HAS(c.kShapes, SAIL_CUBE) && p.type == SAIL_CUBE) ||
+               (HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX))) {
+    boxHit(c, p, r, best, h, HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX);
+  } else
   switch (p.type) {
-    case SAIL_CUBE: if (HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
+    case SAIL_CUBE: if (!boxU && HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
     case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) { rectHit(c, p, RECOMP_HL ? rectLocalHit(p, r, best) : sw.bhl, h); break; } __builtin_unreachable();
     case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, BHL, h); break; } __builtin_unreachable();
@@ -1055,7 +1095,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
     case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, BHL, h); break; } __builtin_unreachable();
-    case SAIL_CORNELLBOX: if (HAS(c.kShapes, SAIL_CORNELLBOX)) { cornellHit(p, r, best, h); break; } __builtin_unreachable();
+    case SAIL_CORNELLBOX: if (!boxU && HAS(c.kShapes, SAIL_CORNELLBOX)) { cornellHit(p, r, best, h); break; } __builtin_unreachable();
     default: __builtin_unreachable();
   }
 #undef BHL
