@@ -455,7 +455,9 @@ D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
 #ifndef SAIL_BOX_UNIFIED
 #define SAIL_BOX_UNIFIED 2
 #endif
-#define SAIL_BOX_UNIFIED_ON(ks) (SAIL_BOX_UNIFIED == 1 || (SAIL_BOX_UNIFIED == 2 && (ks) == SAIL_KSET_ROOM_SHAPES))
+// 3 = only in waves whose lanes won different rows (hitRecordU's non-uniform path), 4 = 3 plus every room-kernel wave
+#define SAIL_BOX_UNIFIED_ON(ks) \
+  (SAIL_BOX_UNIFIED == 1 || ((SAIL_BOX_UNIFIED == 2 || SAIL_BOX_UNIFIED == 4) && (ks) == SAIL_KSET_ROOM_SHAPES))
 D void boxHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h, bool cornell) {
   h.hit = r.o + t * r.d;
   const float s = cornell ? -1.0f : sgn(p.rev);
@@ -1070,7 +1072,8 @@ D V3 rectLocalHit(const SailPrim& p, const Ray& r, float t) {
   const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
   return o + t * d;
 }
-template <bool RECOMP_HL = false>
+// MIXED: the record of a wave whose lanes won different rows (hitRecordU), where SAIL_BOX_UNIFIED 3 / 4 share the box code
+template <bool RECOMP_HL = false, bool MIXED = false>
 D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const float best = sw.best;
   const int bi = sw.bi;
@@ -1081,7 +1084,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // zero default would be materialised for every lane before the dispatch
   const SailPrim& p = c.rowCopy ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
-  const bool boxU = SAIL_BOX_UNIFIED_ON(c.kShapes);  // a compile-time constant in each kernel
+  const bool boxU = SAIL_BOX_UNIFIED_ON(c.kShapes) || (SAIL_BOX_UNIFIED >= 3 && MIXED);  // compile-time constant
   if (boxU && ((HAS(c.kShapes, SAIL_CUBE) && p.type == SAIL_CUBE) ||
                (HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX))) {
     boxHit(c, p, r, best, h, HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX);
@@ -1127,7 +1130,7 @@ D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
     return hitRecord<RECOMP_HL>(c, r, su);
   }
 #endif
-  return hitRecord<RECOMP_HL>(c, r, sw);
+  return hitRecord<RECOMP_HL, true>(c, r, sw);
 }
 D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc) {
   const Sweep sw = sweepRay(c, r, primary);
