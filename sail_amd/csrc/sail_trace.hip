@@ -281,6 +281,12 @@ D V2 concentricSampleDisk(V2 u) {
 }
 
 // ---- textures (shader.texture.js:22-29) ----------------------------------------------------------------
+// SAIL_TEX_SHARED: the two checkerboards share uv / size and its floor, so a wave holding both runs them once (same
+// operations). Measured (bit-identical, profiles/r03_variants_tex_shared.jsonl, three rounds): C3 -1.4 %, C4 +0.7 %
+// (its 64 rows mix both textures in most waves): 2 (default) = the pre-cull kernels only, 1 = every kernel, 0 = off.
+#ifndef SAIL_TEX_SHARED
+#define SAIL_TEX_SHARED 2
+#endif
 // UNIFORM_COLOR ignores uv, so hit records skip the UV arithmetic (atan2/acos/divides) for it
 D int matCat(const SailPrim& p) { return (int)(short)(p.cats & 0xffff); }
 D int texCat(const SailPrim& p) { return p.cats >> 16; }
@@ -289,6 +295,22 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, const SailPrim& p) {
   const int texRow = p.texRow, cat = texCat(p);
   if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
   if (cat < 0 || cat >= 32 || !((c.texMask >> cat) & 1u)) return v3s(0.0f);
+  // c.cullPrims is a compile-time constant in every kernel (the pre-cull ones set 1)
+  if ((SAIL_TEX_SHARED == 1 || (SAIL_TEX_SHARED == 2 && c.cullPrims)) &&
+      ((cat == SAIL_TEX_CHECKERBOARD && HAS(c.kTex, SAIL_TEX_CHECKERBOARD)) ||
+       (cat == SAIL_TEX_CHECKERBOARD2 && HAS(c.kTex, SAIL_TEX_CHECKERBOARD2)))) {
+    const bool cb1 = cat == SAIL_TEX_CHECKERBOARD;
+    const float size = cb1 ? TP(c, texRow, 1) : TP(c, texRow, 7);
+    const float sx = fdiv(uv.x, size), sy = fdiv(uv.y, size);
+    const float qx = floorf(sx), qy = floorf(sy);
+    if (cb1) {
+      const float width = fdiv(0.5f * TP(c, texRow, 2), size);
+      const float fx = sx - qx, fy = sy - qy;
+      const bool in_outline = (fx < width || fx > 1.0f - width) || (fy < width || fy > 1.0f - width);
+      return in_outline ? v3s(0.5f) : v3s(1.0f);
+    }
+    return (to_int(qx + qy) % 2 == 0) ? TP3(c, texRow, 1) : TP3(c, texRow, 4);
+  }
   switch (cat) {
     case SAIL_TEX_CHECKERBOARD: if (!HAS(c.kTex, SAIL_TEX_CHECKERBOARD)) break; {
       const float size = TP(c, texRow, 1), lineWidth = TP(c, texRow, 2);
