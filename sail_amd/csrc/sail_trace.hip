@@ -787,6 +787,103 @@ D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const V3 dpdv = v3(hit.x, hit.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
+// SAIL_LOCAL_SHARED: one hit record for the six local-space shapes (sphere, cone, cylinder, hyperboloid, paraboloid,
+// disk). Each computes the same tail -- the azimuth phiOf (atan2) of its UV, dpdu = dpduRot(hit), a normalised cross,
+// the texture and four local-to-world transforms -- so a wave whose lanes hit different shape types (the pre-cull
+// kernel sorts by material, then shape) runs that tail once instead of once per type. Per type only the phi
+// arguments, the v coordinate, dpdv and the cross order differ. Same operations on the same values as sphereHit and
+// the finishLocal callers above. 1 = every kernel, 2 = the pre-cull kernels, 3 = the pre-cull kernels' waves whose
+// lanes won different rows, 0 = off. Measured (bit-identical, profiles/r03_variants_local_shared.jsonl, three rounds):
+// 2 C4 +3.3 %, C2/C3 unchanged; 3 C4 +3.2 %; 1 C4 +3.1 %, C3 -0.8 %. Default 2.
+#ifndef SAIL_LOCAL_SHARED
+#define SAIL_LOCAL_SHARED 2
+#endif
+D bool isLocalShape(int t) {
+  return t == SAIL_SPHERE || t == SAIL_CONE || t == SAIL_CYLINDER || t == SAIL_HYPERBOLOID || t == SAIL_PARABOLOID ||
+         t == SAIL_DISK;
+}
+D void localHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
+  const int ty = p.type;
+  const bool nUV = needsUV(p);
+  // the azimuth's arguments: (y, x) of the hit, the sphere's pole guard, the hyperboloid's rotated frame
+  float py = hl.y, px = hl.x, theta = 0.0f, hv = 0.0f;
+  V3 p1 = v3s(0.0f), p2 = v3s(0.0f);
+  bool needPhi = nUV;
+  if (ty == SAIL_SPHERE) {
+    theta = acosf_(clamp_(fdiv(hl.z, p.a[3]), -1.0f, 1.0f));
+    if (hl.x == 0.0f && hl.y == 0.0f) px = 1e-5f * p.a[3];
+  } else if (ty == SAIL_HYPERBOLOID) {
+    p1 = P3(p, 3); p2 = P3(p, 6);
+    hv = fdiv(hl.z - p1.z, p2.z - p1.z);
+    const V3 pr = (1.0f - hv) * p1 + hv * p2;
+    py = pr.x * hl.y - hl.x * pr.y; px = hl.x * pr.x + hl.y * pr.y;
+    needPhi = true;
+  }
+  float phi = 0.0f, u = 0.0f;
+  if (needPhi) { phi = phiOf(py, px); u = fdiv(phi, 2.0f * kPI); }
+  V2 uv = v2(0.0f, 0.0f);
+  const V3 dpdu = dpduRot(hl);
+  V3 dpdv, nc;
+  switch (ty) {
+    case SAIL_SPHERE: {
+      const float rad = p.a[3];
+      if (nUV) uv = v2(u, fdiv(theta, kPI));
+      const float zRadius = sqrtf_(hl.x * hl.x + hl.y * hl.y);
+      const float invZRadius = rcp_rn(zRadius);
+      const float cosPhi = hl.x * invZRadius, sinPhi = hl.y * invZRadius;
+      dpdv = kPI * v3(hl.z * cosPhi, hl.z * sinPhi, -rad * sinf_(theta));
+      nc = crossZb(dpdv, dpdu);
+      break;
+    }
+    case SAIL_CONE: {
+      const float hh = p.a[3];
+      if (nUV) uv = v2(u, fdiv(hl.z, hh));
+      const float vv = fdiv(hl.z, hh);
+      dpdv = v3(fdiv(-hl.x, 1.0f - vv), fdiv(-hl.y, 1.0f - vv), hh);
+      nc = crossZa(dpdu, dpdv);
+      break;
+    }
+    case SAIL_CYLINDER: {
+      const float hh = p.a[3];
+      if (nUV) uv = v2(u, fdiv(hl.z, hh));
+      dpdv = v3(0.0f, 0.0f, hh);
+      nc = crossZa(dpdu, dpdv);
+      break;
+    }
+    case SAIL_HYPERBOLOID: {
+      uv = v2(u, hv);
+      float sinPhi, cosPhi; sincosf_(phi, sinPhi, cosPhi);
+      dpdv = v3((p2.x - p1.x) * cosPhi - (p2.y - p1.y) * sinPhi, (p2.x - p1.x) * sinPhi + (p2.y - p1.y) * cosPhi, p2.z - p1.z);
+      nc = crossZa(dpdu, dpdv);
+      break;
+    }
+    case SAIL_PARABOLOID: {
+      const float zMin = fmin_(p.a[3], p.a[4]), zMax = fmax_(p.a[3], p.a[4]);
+      if (nUV) uv = v2(u, fdiv(hl.z - zMin, zMax - zMin));
+      dpdv = (zMax - zMin) * v3(fdiv(hl.x, 2.0f * hl.z), fdiv(hl.y, 2.0f * hl.z), 1.0f);
+      nc = crossZa(dpdu, dpdv);
+      break;
+    }
+    default: {  // SAIL_DISK
+      const float rad = p.a[3], ri = p.a[4];
+      const float dist2 = hl.x * hl.x + hl.y * hl.y;
+      if (nUV) {
+        const float rHit = sqrtf_(dist2);
+        const float oneMinusV = fdiv(rHit - ri, rad - ri);
+        uv = v2(u, 1.0f - oneMinusV);
+      }
+      dpdv = v3(hl.x, hl.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
+      nc = crossZa(dpdu, dpdv);
+      break;
+    }
+  }
+  const V3 nl = normalize(nc);
+  h.sc = getSurfaceColor(c, uv, p);
+  h.hit = L2W(hl) + P3(p, 0);
+  h.normal = L2W(nl);
+  h.dpdu = L2W(dpdu);
+  h.dpdv = L2W(dpdv);
+}
 
 // hl (may be null): the local-space hit point of the shapes whose hit record starts from it
 D float primT(const Ctx& c, const SailPrim& p, const Ray& r, V3* hl) {
@@ -1107,19 +1204,25 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const SailPrim& p = c.rowCopy ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
   const bool boxU = SAIL_BOX_UNIFIED_ON(c.kShapes) || (SAIL_BOX_UNIFIED >= 3 && MIXED);  // compile-time constant
+  const bool localU = SAIL_LOCAL_SHARED == 1 || (SAIL_LOCAL_SHARED == 2 && c.cullPrims) ||
+                      (SAIL_LOCAL_SHARED == 3 && c.cullPrims && MIXED);
+  const uint32_t kLocal = c.kShapes & ((1u << SAIL_SPHERE) | (1u << SAIL_CONE) | (1u << SAIL_CYLINDER) |
+                                       (1u << SAIL_HYPERBOLOID) | (1u << SAIL_PARABOLOID) | (1u << SAIL_DISK));
   if (boxU && ((HAS(c.kShapes, SAIL_CUBE) && p.type == SAIL_CUBE) ||
                (HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX))) {
     boxHit(c, p, r, best, h, HAS(c.kShapes, SAIL_CORNELLBOX) && p.type == SAIL_CORNELLBOX);
+  } else if (localU && ((kLocal >> p.type) & 1u)) {
+    localHit(c, p, BHL, h);
   } else
   switch (p.type) {
     case SAIL_CUBE: if (!boxU && HAS(c.kShapes, SAIL_CUBE)) { cubeHit(c, p, r, best, h); break; } __builtin_unreachable();
-    case SAIL_SPHERE: if (HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_SPHERE: if (!localU && HAS(c.kShapes, SAIL_SPHERE)) { sphereHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_RECTANGLE: if (HAS(c.kShapes, SAIL_RECTANGLE)) { rectHit(c, p, RECOMP_HL ? rectLocalHit(p, r, best) : sw.bhl, h); break; } __builtin_unreachable();
-    case SAIL_CONE: if (HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, BHL, h); break; } __builtin_unreachable();
-    case SAIL_CYLINDER: if (HAS(c.kShapes, SAIL_CYLINDER)) { cylinderHit(c, p, BHL, h); break; } __builtin_unreachable();
-    case SAIL_DISK: if (HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, BHL, h); break; } __builtin_unreachable();
-    case SAIL_HYPERBOLOID: if (HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, BHL, h); break; } __builtin_unreachable();
-    case SAIL_PARABOLOID: if (HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_CONE: if (!localU && HAS(c.kShapes, SAIL_CONE)) { coneHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_CYLINDER: if (!localU && HAS(c.kShapes, SAIL_CYLINDER)) { cylinderHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_DISK: if (!localU && HAS(c.kShapes, SAIL_DISK)) { diskHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_HYPERBOLOID: if (!localU && HAS(c.kShapes, SAIL_HYPERBOLOID)) { hypHit(c, p, BHL, h); break; } __builtin_unreachable();
+    case SAIL_PARABOLOID: if (!localU && HAS(c.kShapes, SAIL_PARABOLOID)) { paraHit(c, p, BHL, h); break; } __builtin_unreachable();
     case SAIL_CORNELLBOX: if (!boxU && HAS(c.kShapes, SAIL_CORNELLBOX)) { cornellHit(p, r, best, h); break; } __builtin_unreachable();
     default: __builtin_unreachable();
   }
