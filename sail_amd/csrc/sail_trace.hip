@@ -727,6 +727,74 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
   if (hitOut) *hitOut = hit;
   return t;
 }
+// SAIL_QUAD_SHARED: the pre-cull kernel's candidate sweep tests cones, cylinders, hyperboloids and paraboloids in one
+// loop (quadT) instead of one loop per type. A wave then runs max-over-lanes(quadric candidates) iterations instead
+// of the sum over the four types of max-over-lanes(candidates of the type). Per type only the coefficients and the
+// z-range / box parameters differ; the ray transform, the root solve, rootPick and the box test are shared. Same
+// operations on the same values as coneT / cylinderT / hypT / paraT (box test last, SAIL_BOX_LAST). Candidates are
+// visited out of row order either way (the take rule keeps the in-order winner).
+// Measured (bit-identical, profiles/r03_variants_quad_shared.jsonl, three rounds): C4 +0.9 %. 1 (default) = the four
+// quadrics, 2 = the sphere too (its own root rule), 0 = one loop per type.
+#ifndef SAIL_QUAD_SHARED
+#define SAIL_QUAD_SHARED 1
+#endif
+D bool isQuadric(int t) {
+  return t == SAIL_CONE || t == SAIL_CYLINDER || t == SAIL_HYPERBOLOID || t == SAIL_PARABOLOID;
+}
+D float quadT(const SailPrim& p, const Ray& r0, V3* hitOut) {
+  const int ty = p.type;
+  const V3 pp = P3(p, 0);
+  const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
+  float a, b, cc, zlo, zhi, bA, bB, bC;
+  bool epsLo;
+  if (SAIL_QUAD_SHARED >= 2 && ty == SAIL_SPHERE) {  // sphereT (sphere.glsl:45-86)
+    const float rad = p.a[3];
+    const float sa = dot(d, d), sb = 2.0f * dot(o, d), sc = dot(o, o) - rad * rad;
+    float t1 = 0.0f, t2 = 0.0f;
+    if (!quadratic(sa, sb, sc, t1, t2)) return kMaxDistance;
+    if (t2 < kEps) return kMaxDistance;
+    float t = t1;
+    if (t1 < kEps) t = t2;
+    if (t >= kMaxDistance) return kMaxDistance;
+    if (!testBoundbox(r0, pp - v3s(rad), pp + v3s(rad))) return kMaxDistance;
+    if (hitOut) *hitOut = o + t * d;
+    return t;
+  }
+  if (ty == SAIL_CONE) {
+    const float h = p.a[3], rad = p.a[4], k = p.a[5];
+    a = d.x * d.x + d.y * d.y - k * d.z * d.z;
+    b = 2.0f * (d.x * o.x + d.y * o.y - k * d.z * (o.z - h));
+    cc = o.x * o.x + o.y * o.y - k * (o.z - h) * (o.z - h);
+    zlo = 0.0f; zhi = h; epsLo = true; bA = rad; bB = 0.0f; bC = h;
+  } else if (ty == SAIL_CYLINDER) {
+    const float h = p.a[3], rad = p.a[4];
+    a = d.x * d.x + d.y * d.y;
+    b = 2.0f * (d.x * o.x + d.y * o.y);
+    cc = o.x * o.x + o.y * o.y - rad * rad;
+    zlo = 0.0f; zhi = h; epsLo = true; bA = rad; bB = 0.0f; bC = h;
+  } else if (ty == SAIL_HYPERBOLOID) {
+    const float ah = p.a[9], ch = p.a[10];
+    a = ah * d.x * d.x + ah * d.y * d.y - ch * d.z * d.z;
+    b = 2.0f * (ah * d.x * o.x + ah * d.y * o.y - ch * d.z * o.z);
+    cc = ah * o.x * o.x + ah * o.y * o.y - ch * o.z * o.z - 1.0f;
+    zlo = p.a[12]; zhi = p.a[13]; epsLo = false; bA = p.a[11]; bB = -p.a[12]; bC = p.a[13];
+  } else {  // SAIL_PARABOLOID
+    const float z0 = p.a[3], z1 = p.a[4], rad = p.a[5];
+    const float zMin = fmin_(z0, z1), zMax = fmax_(z0, z1);
+    const float k = p.a[6];
+    a = k * (d.x * d.x + d.y * d.y);
+    b = 2.0f * k * (d.x * o.x + d.y * o.y) - d.z;
+    cc = k * (o.x * o.x + o.y * o.y) - o.z;
+    zlo = zMin; zhi = zMax; epsLo = false; bA = rad; bB = -zMin; bC = zMax;
+  }
+  float t1 = 0.0f, t2 = 0.0f, t; V3 hit;
+  if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
+  if (t2 < -kEps) return kMaxDistance;
+  if (!rootPick(t1, t2, o, d, zlo, zhi, epsLo, t, hit)) return kMaxDistance;
+  if (!testBoundbox(r0, pp - v3(bA, bB, bA), pp + v3(bA, bC, bA))) return kMaxDistance;
+  if (hitOut) *hitOut = hit;
+  return t;
+}
 // local-space tail shared by the quadrics and the disk: normal from dpdu x dpdv, texture, back to world
 // dpdu is dpduRot(hit) for every caller (z == 0)
 D void finishLocal(const Ctx& c, const SailPrim& p, V3 hl, V2 uv, V3 dpdu, V3 dpdv, Hit& h) {
@@ -1099,6 +1167,36 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
     }
   }
 }
+// the four quadric types' candidates in one loop (SAIL_QUAD_SHARED)
+template <bool HIT>
+D void candQuad(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
+  const uint32_t kq = c.kShapes & ((1u << SAIL_CONE) | (1u << SAIL_CYLINDER) | (1u << SAIL_HYPERBOLOID) |
+                                   (1u << SAIL_PARABOLOID) | (SAIL_QUAD_SHARED >= 2 ? (1u << SAIL_SPHERE) : 0u));
+  if (kq == 0u) return;
+  const unsigned long long* tms = c.typeMasks + (base >> 6) * 16;
+  unsigned long long tm = 0ull;
+  if (HAS(kq, SAIL_CONE)) tm |= constRow<unsigned long long>(tms, SAIL_CONE);
+  if (HAS(kq, SAIL_CYLINDER)) tm |= constRow<unsigned long long>(tms, SAIL_CYLINDER);
+  if (HAS(kq, SAIL_HYPERBOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_HYPERBOLOID);
+  if (HAS(kq, SAIL_PARABOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_PARABOLOID);
+  if (HAS(kq, SAIL_SPHERE)) tm |= constRow<unsigned long long>(tms, SAIL_SPHERE);
+  unsigned long long m = cand & tm;
+  while (__ballot(m != 0ull)) {
+    if (m != 0ull) {
+      const int i = base + __builtin_ctzll(m);
+      m &= m - 1ull;
+      const SailPrim& p = c.cprims[i];
+      if (HIT || !SAIL_SHADOW_T_ONLY) {
+        V3 hl = v3s(0.0f);
+        const float t = quadT(p, r, &hl);
+        if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
+      } else {
+        const float t = quadT(p, r, nullptr);
+        if (t < best) best = t;
+      }
+    }
+  }
+}
 // limit: the pre-cull distance bound before any hit (kMaxDistance, or 1 for shadow rays: see closestT)
 template <bool HIT>
 D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, V3& bhl) {
@@ -1112,11 +1210,17 @@ D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, 
     candType<SAIL_CORNELLBOX, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_RECTANGLE, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_DISK, HIT>(c, r, base, cand, best, bi, bhl);
+#if !(SAIL_QUAD_SHARED >= 2 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
     candType<SAIL_SPHERE, HIT>(c, r, base, cand, best, bi, bhl);
+#endif
+#if SAIL_QUAD_SHARED && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL
+    candQuad<HIT>(c, r, base, cand, best, bi, bhl);
+#else
     candType<SAIL_CYLINDER, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_CONE, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_PARABOLOID, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_HYPERBOLOID, HIT>(c, r, base, cand, best, bi, bhl);
+#endif
   }
 }
 
