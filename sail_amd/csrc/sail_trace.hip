@@ -1375,14 +1375,15 @@ D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc)
 }
 
 // ---- sampleGeometry for area lights (shader.shape.js:53-67) -----------------------------------------------------
-D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
+// qs (may be null): uniformSampleSphere(u), already computed by the caller (SAIL_LIGHT_SHARED)
+D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf, const V3* qs = nullptr) {
   normal = v3s(0.0f);
   pdf = 0.0f;
   const SailPrim& p = c.rowCopy ? c.cprims[row] : PRIM(c, row);
   const float s = sgn(p.rev);
   switch (p.type) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
-      const V3 q = uniformSampleSphere(u);
+      const V3 q = qs ? *qs : uniformSampleSphere(u);
       const float rad = p.a[3];
       pdf = fdiv(kInvPI, rad * rad);
       const V3 res = q * rad + P3(p, 0);
@@ -1652,6 +1653,11 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
 }
 
 // ---- lights (shader.light.js:12-22, light/*.glsl) ---------------------------------------------------------------
+// study switch (bit-identical, profiles/r03_variants_light_shared.jsonl): C4 -0.35 % -- the extra light-row read and the
+// hoisted sample cost more than the second evaluation it saves -- so 0 (off)
+#ifndef SAIL_LIGHT_SHARED
+#define SAIL_LIGHT_SHARED 0
+#endif
 D bool testShadow(const Ctx& c, const Ray& r) {
   const float d = closestT(c, r);
   return d > kEps && d < kOneMinusEps;
@@ -1677,17 +1683,26 @@ D LightPrep lightPrep(const Ctx& c, const Hit& ins, V2 u2) {
   const float* L = c.lt + row * 18;
   V3 contrib = v3s(0.0f), toLight = v3s(0.0f);
   bool lit = false;
+  // SAIL_LIGHT_SHARED (pre-cull kernels): the sphere direction sample of a point light and of a sphere area light is
+  // the same uniformSampleSphere(u2), evaluated once for the wave's lanes of both kinds
+  const bool lshared = SAIL_LIGHT_SHARED && c.cullPrims && HAS(c.kLights, SAIL_POINT) && HAS(c.kLights, SAIL_AREA) &&
+                       HAS(c.kShapes, SAIL_SPHERE);
+  V3 usph = v3s(0.0f);
+  if (lshared && (cat == SAIL_POINT ||
+                  (cat == SAIL_AREA &&
+                   (c.rowCopy ? c.cprims[c.lightObjRow[row]] : PRIM(c, c.lightObjRow[row])).type == SAIL_SPHERE)))
+    usph = uniformSampleSphere(u2);
   if (cat == SAIL_AREA && HAS(c.kLights, SAIL_AREA)) {  // light/area.glsl
     const V3 em = v3(L[2], L[3], L[4]);
     V3 normal; float pdf;
-    const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
+    const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf, lshared ? &usph : nullptr);
     toLight = p - ins.hit;
     const V3 nt = normalize(toLight);
     contrib = em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
     lit = true;
   } else if (cat == SAIL_POINT && HAS(c.kLights, SAIL_POINT)) {  // light/point.glsl:13-20
     const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
-    const V3 p = from + uniformSampleSphere(u2) * 0.1f;
+    const V3 p = from + (lshared ? usph : uniformSampleSphere(u2)) * 0.1f;
     toLight = p - ins.hit;
     contrib = em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
     lit = true;
