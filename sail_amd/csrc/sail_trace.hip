@@ -734,7 +734,7 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
 // operations on the same values as coneT / cylinderT / hypT / paraT (box test last, SAIL_BOX_LAST). Candidates are
 // visited out of row order either way (the take rule keeps the in-order winner).
 // Measured (bit-identical, profiles/r03_variants_quad_shared.jsonl, three rounds): C4 +0.9 %. 1 (default) = the four
-// quadrics, 2 = the sphere too (its own root rule), 0 = one loop per type.
+// quadrics, 2 = the sphere too (its own root rule), 3 = the disk too (planar), 0 = one loop per type.
 #ifndef SAIL_QUAD_SHARED
 #define SAIL_QUAD_SHARED 1
 #endif
@@ -747,7 +747,19 @@ D float quadT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   float a, b, cc, zlo, zhi, bA, bB, bC;
   bool epsLo;
-  if (SAIL_QUAD_SHARED >= 2 && ty == SAIL_SPHERE) {  // sphereT (sphere.glsl:45-86)
+  if (SAIL_QUAD_SHARED == 3 && ty == SAIL_DISK) {  // diskT (disk.glsl:36-75)
+    const float rad = p.a[3], ri = p.a[4];
+    if (d.z == 0.0f) return kMaxDistance;
+    const float t = fdiv(-o.z, d.z);
+    if (t <= 0.0f) return kMaxDistance;
+    const V3 hit = o + t * d;
+    const float dist2 = hit.x * hit.x + hit.y * hit.y;
+    if (dist2 > rad * rad || dist2 < ri * ri) return kMaxDistance;
+    if (t >= kMaxDistance) return kMaxDistance;
+    if (hitOut) *hitOut = hit;
+    return t;
+  }
+  if (SAIL_QUAD_SHARED == 2 && ty == SAIL_SPHERE) {  // sphereT (sphere.glsl:45-86)
     const float rad = p.a[3];
     const float sa = dot(d, d), sb = 2.0f * dot(o, d), sc = dot(o, o) - rad * rad;
     float t1 = 0.0f, t2 = 0.0f;
@@ -1171,7 +1183,8 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
 template <bool HIT>
 D void candQuad(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
   const uint32_t kq = c.kShapes & ((1u << SAIL_CONE) | (1u << SAIL_CYLINDER) | (1u << SAIL_HYPERBOLOID) |
-                                   (1u << SAIL_PARABOLOID) | (SAIL_QUAD_SHARED >= 2 ? (1u << SAIL_SPHERE) : 0u));
+                                   (1u << SAIL_PARABOLOID) | (SAIL_QUAD_SHARED == 2 ? (1u << SAIL_SPHERE) : 0u) |
+                                   (SAIL_QUAD_SHARED == 3 ? (1u << SAIL_DISK) : 0u));
   if (kq == 0u) return;
   const unsigned long long* tms = c.typeMasks + (base >> 6) * 16;
   unsigned long long tm = 0ull;
@@ -1180,6 +1193,7 @@ D void candQuad(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
   if (HAS(kq, SAIL_HYPERBOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_HYPERBOLOID);
   if (HAS(kq, SAIL_PARABOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_PARABOLOID);
   if (HAS(kq, SAIL_SPHERE)) tm |= constRow<unsigned long long>(tms, SAIL_SPHERE);
+  if (HAS(kq, SAIL_DISK)) tm |= constRow<unsigned long long>(tms, SAIL_DISK);
   unsigned long long m = cand & tm;
   while (__ballot(m != 0ull)) {
     if (m != 0ull) {
@@ -1209,8 +1223,10 @@ D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, 
     candType<SAIL_CUBE, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_CORNELLBOX, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_RECTANGLE, HIT>(c, r, base, cand, best, bi, bhl);
+#if !(SAIL_QUAD_SHARED == 3 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
     candType<SAIL_DISK, HIT>(c, r, base, cand, best, bi, bhl);
-#if !(SAIL_QUAD_SHARED >= 2 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
+#endif
+#if !(SAIL_QUAD_SHARED == 2 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
     candType<SAIL_SPHERE, HIT>(c, r, base, cand, best, bi, bhl);
 #endif
 #if SAIL_QUAD_SHARED && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL
