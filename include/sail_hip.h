@@ -163,7 +163,10 @@ int sail_save_accum(sail_ctx* ctx, int part, float* sums, uint64_t* k);
 /* replace accumulator `part` by `sums` and set the sample index to k (every part of the context). part = -1 loads a
  * whole-frame accumulator (sail_read_accum of a reduced frame): on a multi-device context each device keeps its own
  * tiles of it (tile partition) or device 0 takes all of it (sample partition: equal to the uninterrupted render to
- * summation order only; load the parts for bit-exactness). The AOVs restart with the next sample. */
+ * summation order only; load the parts for bit-exactness). The AOVs restart with the next sample. On a multi-device
+ * context a part-wise load must be followed by every other part with the same k: until then rendering, reading,
+ * filtering, saving and reducing fail with SAIL_E_STATE (sail_reset abandons the half-loaded checkpoint), and a part
+ * with a different k fails with SAIL_E_INVALID. The caller checks the sums' size: W*H*4 floats. */
 int sail_load_accum(sail_ctx* ctx, int part, const float* sums, uint64_t k);
 
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */

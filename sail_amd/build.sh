@@ -1,14 +1,21 @@
 #!/bin/sh
 # Builds libsail_hip.so for gfx950 in-tree (sail_amd/lib/). Contraction is off everywhere: the
 # kernels follow the reference's f32 expression order and the bit-defined math spec (sail_math.h).
+# Also builds libsail_hip_phase.so, the same library with per-phase wave timers (-DSAIL_PHASE_TIMING=1,
+# tools/phase_profile.py); tests/test_gpu_parity.py checks that it renders the same bits.
 set -e
 cd "$(dirname "$0")"
 mkdir -p lib build
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 ARCH=${SAIL_ARCH:-gfx950}
 COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function"
-$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_trace.hip -o build/sail_trace.o ${SAIL_EXTRA:-}
-$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_capi.cpp -o build/sail_capi.o
-$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_hostmath.cpp -o build/sail_hostmath.o
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_trace.hip -o build/sail_trace.o ${SAIL_EXTRA:-} &
+$HIPCC $COMMON --offload-arch=$ARCH -DSAIL_PHASE_TIMING=1 -c csrc/sail_trace.hip -o build/sail_trace_phase.o &
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_capi.cpp -o build/sail_capi.o &
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_hostmath.cpp -o build/sail_hostmath.o &
+wait
+for o in build/sail_trace.o build/sail_trace_phase.o build/sail_capi.o build/sail_hostmath.o; do [ -s $o ] || { echo "missing $o"; exit 1; }; done
 $HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o build/sail_capi.o build/sail_hostmath.o \
   -o lib/libsail_hip.so -ldl
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace_phase.o build/sail_capi.o build/sail_hostmath.o \
+  -o lib/libsail_hip_phase.so -ldl

@@ -265,6 +265,8 @@ class Context:
         if rc:
             raise SailError(f"{what}: {rc}: {self.lib.sail_last_error(None).decode()}")
         self.h = h
+        self._accum_mode = ACCUM_SUM          # the C ABI's default (sail_create)
+        self._partition = (0, 1, PART_TILES)  # (rank, world, mode): checkpoints record and check these
         for opt, val in {**DEBUG_DEFAULTS, **(debug or {})}.items():
             self.set_debug(opt, val)
 
@@ -298,9 +300,11 @@ class Context:
 
     def set_accum_mode(self, mode: int):
         self._check(self.lib.sail_set_accum_mode(self.h, mode), "sail_set_accum_mode")
+        self._accum_mode = int(mode)
 
     def set_partition(self, rank: int, world: int, mode: int = PART_TILES):
         self._check(self.lib.sail_set_partition(self.h, rank, world, mode), "sail_set_partition")
+        self._partition = (int(rank), int(world), int(mode))
 
     def set_launch_samples(self, spp: int):
         self._check(self.lib.sail_set_launch_samples(self.h, spp), "sail_set_launch_samples")
@@ -372,26 +376,46 @@ class Context:
     def reduce(self, root: int = 0):
         self._check(self.lib.sail_reduce(self.h, root), "sail_reduce")
 
-    def save(self) -> dict:
-        """Checkpoint of the progressive render: {"k": next sample index, "parts": [W x H x 4 f32 accumulator per
-        device]} (sail_save_accum)"""
+    def _parts(self) -> int:
         n = ctypes.c_int(0)
         self._check(self.lib.sail_accum_parts(self.h, ctypes.byref(n)), "sail_accum_parts")
+        return n.value
+
+    def save(self) -> dict:
+        """Checkpoint of the progressive render: {"k": next sample index, "parts": [H x W x 4 f32 accumulator per
+        device], and the context it belongs to: width, height, accum_mode, partition (rank, world, mode)}
+        (sail_save_accum)"""
         parts, k = [], ctypes.c_uint64(0)
-        for i in range(n.value):
+        for i in range(self._parts()):
             a = np.zeros((self.H, self.W, 4), dtype=np.float32)
             self._check(self.lib.sail_save_accum(self.h, i, _ptr(a), ctypes.byref(k)), "sail_save_accum")
             parts.append(a)
-        return {"k": int(k.value), "parts": parts}
+        return {"k": int(k.value), "parts": parts, "width": self.W, "height": self.H,
+                "accum_mode": self._accum_mode, "partition": list(self._partition)}
 
     def load(self, ckpt: dict):
-        """Resume from save()'s checkpoint (every part), or from a whole-frame accumulator
-        {"k": k, "frame": W x H x 4} (sail_load_accum part -1)"""
+        """Resume from save()'s checkpoint (every part, into a context of the same size, accumulation mode, partition
+        and device count), or from a whole-frame accumulator {"k": k, "frame": H x W x 4} (sail_load_accum part -1).
+        A checkpoint that does not fit this context raises SailError before anything is copied."""
+        def arr(a, what):
+            a = _f32(a)
+            if a.shape != (self.H, self.W, 4):
+                raise SailError(f"Context.load: {what} has shape {a.shape}, this context needs {(self.H, self.W, 4)}")
+            return a
+        for key, mine in (("width", self.W), ("height", self.H), ("accum_mode", self._accum_mode)):
+            if key in ckpt and int(ckpt[key]) != mine:
+                raise SailError(f"Context.load: checkpoint {key} {ckpt[key]} differs from this context's {mine}")
+        if "partition" in ckpt and tuple(int(v) for v in ckpt["partition"]) != self._partition:
+            raise SailError(f"Context.load: checkpoint partition {tuple(ckpt['partition'])} differs from {self._partition}")
         if "frame" in ckpt:
-            self._check(self.lib.sail_load_accum(self.h, -1, _ptr(_f32(ckpt["frame"])), int(ckpt["k"])), "sail_load_accum")
+            f = arr(ckpt["frame"], "frame")
+            self._check(self.lib.sail_load_accum(self.h, -1, _ptr(f), int(ckpt["k"])), "sail_load_accum")
             return
-        for i, a in enumerate(ckpt["parts"]):
-            self._check(self.lib.sail_load_accum(self.h, i, _ptr(_f32(a)), int(ckpt["k"])), "sail_load_accum")
+        parts = [arr(a, f"part {i}") for i, a in enumerate(ckpt["parts"])]
+        if len(parts) != self._parts():
+            raise SailError(f"Context.load: checkpoint has {len(parts)} parts, this context {self._parts()}")
+        for i, a in enumerate(parts):
+            self._check(self.lib.sail_load_accum(self.h, i, _ptr(a), int(ckpt["k"])), "sail_load_accum")
 
     def accum_device_ptr(self):
         p = ctypes.c_void_p()

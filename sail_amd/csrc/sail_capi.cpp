@@ -170,6 +170,11 @@ struct sail_ctx {
   // partition on its own stream; `dirty` = rendered since the last reduce. Devices are all distinct (grouped
   // RCCL reduce over a ncclCommInitAll communicator) or all the same one (`groupLocal`: summed by a kernel).
   std::vector<sail_ctx*> subs;
+  // A checkpoint loaded part by part (sail_load_accum part >= 0): the parts still missing (bit i = device i) and the
+  // checkpoint's k. Until every part is in, the frame mixes old and loaded accumulators, so rendering, reading, saving
+  // and reducing are refused.
+  uint64_t loadMissing = 0;
+  uint64_t loadK = 0;
   std::vector<nccl_comm_t> groupComms;
   bool groupLocal = false;
   bool dirty = false;
@@ -196,6 +201,12 @@ int fail(sail_ctx* c, int code, const char* fmt, ...) {
 int relay(sail_ctx* c, int rc, const sail_ctx* sub) {
   if (rc != SAIL_OK && sub && c != sub) c->err = sub->err;
   return rc;
+}
+// a part-wise checkpoint load still missing parts (sail_load_accum): refuse whatever would see the half-loaded frame
+int loadIncomplete(sail_ctx* c, const char* what) {
+  if (!c->loadMissing) return SAIL_OK;
+  return fail(c, SAIL_E_STATE, "%s: checkpoint parts not loaded yet (mask 0x%llx of %d devices); load every part or reset",
+              what, (unsigned long long)c->loadMissing, (int)c->subs.size());
 }
 #define HIPCHK(ctx, call)                                                                       \
   do {                                                                                             \
@@ -1149,7 +1160,9 @@ int sail_set_launch_samples(sail_ctx* c, int spp) {
 
 int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, const float eye[3], int spp, int maxBounces) {
   if (!c) return SAIL_E_INVALID;
-  if (!c->subs.empty()) {  // every device queues its share on its own stream; the host does not wait
+  if (!c->subs.empty()) {
+    // every device queues its share on its own stream; the host does not wait
+    if (int rc = loadIncomplete(c, "sail_render_schedule")) return rc;
     for (sail_ctx* s : c->subs)
       if (int rc = sail_render_schedule(s, inv, seeds, eye, spp, maxBounces)) return relay(c, rc, s);
     c->dirty = true;
@@ -1186,6 +1199,7 @@ int sail_render_schedule(sail_ctx* c, const float* inv, const float* seeds, cons
 int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed, int maxBounces) {
   if (!c) return SAIL_E_INVALID;
   if (!c->subs.empty()) {
+    if (int rc = loadIncomplete(c, "sail_render")) return rc;
     for (sail_ctx* s : c->subs) if (int rc = sail_render(s, inv, eye, seed, maxBounces)) return relay(c, rc, s);
     c->dirty = true;
     return SAIL_OK;
@@ -1219,6 +1233,7 @@ int sail_reset(sail_ctx* c) {
   if (!c->subs.empty()) {
     for (sail_ctx* s : c->subs) if (int rc = sail_reset(s)) return relay(c, rc, s);
     c->dirty = false;
+    c->loadMissing = 0;
     return SAIL_OK;
   }
   HIPCHK(c, hipSetDevice(c->device));
@@ -1241,6 +1256,7 @@ int sail_sync(sail_ctx* c) {
 int sail_read_accum(sail_ctx* c, float* rgba) {
   if (!c || !rgba) return SAIL_E_INVALID;
   if (!c->subs.empty()) {
+    if (int rc = loadIncomplete(c, "sail_read_accum")) return rc;
     if (int rc = groupReduce(c)) return rc;
     return relay(c, sail_read_accum(c->subs[0], rgba), c->subs[0]);
   }
@@ -1253,6 +1269,7 @@ int sail_read_accum(sail_ctx* c, float* rgba) {
 int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
   if (!c) return SAIL_E_INVALID;
   if (!c->subs.empty()) {
+    if (int rc = loadIncomplete(c, "sail_readback")) return rc;
     if (int rc = groupReduce(c)) return rc;
     return relay(c, sail_readback(c->subs[0], rgba, normal, position), c->subs[0]);
   }
@@ -1282,7 +1299,9 @@ int sail_readback(sail_ctx* c, float* rgba, float* normal, float* position) {
 
 int sail_filter(sail_ctx* c, int kind, const float* weights16, float rx, float ry, float gammaC, float* out, uint8_t* out8) {
   if (!c) return SAIL_E_INVALID;
-  if (!c->subs.empty()) {  // the display pass runs on device 0 over the reduced frame
+  if (!c->subs.empty()) {
+    // the display pass runs on device 0 over the reduced frame
+    if (int rc = loadIncomplete(c, "sail_filter")) return rc;
     if (int rc = groupReduce(c)) return rc;
     return relay(c, sail_filter(c->subs[0], kind, weights16, rx, ry, gammaC, out, out8), c->subs[0]);
   }
@@ -1437,6 +1456,7 @@ int sail_reduce(sail_ctx* c, int root) {
   if (!c) return SAIL_E_INVALID;
   if (!c->subs.empty()) {
     if (root != 0) return fail(c, SAIL_E_INVALID, "multi-device context: the frame is reduced into device 0");
+    if (int rc = loadIncomplete(c, "sail_reduce")) return rc;
     c->dirty = true;  // reduce now even if nothing was rendered since the last one
     return groupReduce(c);
   }
@@ -1479,6 +1499,7 @@ int sail_accum_parts(sail_ctx* c, int* parts) {
 int sail_save_accum(sail_ctx* c, int part, float* sums, uint64_t* k) {
   if (!c || !sums || !k) return SAIL_E_INVALID;
   if (!c->subs.empty()) {
+    if (int rc = loadIncomplete(c, "sail_save_accum")) return rc;
     if (part < 0 || part >= (int)c->subs.size()) return fail(c, SAIL_E_INVALID, "sail_save_accum: part %d of %d", part, (int)c->subs.size());
     return relay(c, sail_save_accum(c->subs[part], 0, sums, k), c->subs[part]);
   }
@@ -1494,6 +1515,13 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
   if (!c->subs.empty()) {
     const int nd = (int)c->subs.size();
     if (part < -1 || part >= nd) return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d of %d", part, nd);
+    const uint64_t all = nd >= 64 ? ~0ull : (1ull << nd) - 1ull;
+    if (part >= 0) {  // one part of a checkpoint: the others must follow with the same k before the frame is used
+      if (!c->loadMissing) { c->loadMissing = all; c->loadK = k; }
+      else if (k != c->loadK)
+        return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d has k %llu, the checkpoint being loaded %llu", part,
+                    (unsigned long long)k, (unsigned long long)c->loadK);
+    }
     for (int i = 0; i < nd; i++) {  // part -1: each device keeps its share of the frame; else one part, every k
       if (part == -1 || part == i) {
         if (int rc = sail_load_accum(c->subs[i], part == -1 ? -1 : 0, sums, k)) return relay(c, rc, c->subs[i]);
@@ -1501,6 +1529,7 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
         c->subs[i]->k = k;
       }
     }
+    c->loadMissing = part == -1 ? 0 : (c->loadMissing & ~(1ull << part));
     c->dirty = true;
     return SAIL_OK;
   }

@@ -89,14 +89,11 @@ struct SailWfState {
 // Precompiled plugin-set kernels (bit masks over the ids above). A scene whose plugin masks are subsets of a
 // set's masks may use that set's kernel; everything else runs the generic one.
 enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
-// SAIL_GROUP_HOME: with sample groups, the room kernel's first group adds its samples to the accumulator itself and
-// the other groups stage theirs (C3 +1 %); in the other kernels the extra path costs more registers than the staged
-// samples it saves (C2 -1.4 %, C4 -0.6 %), so every group stages. 0 = every kernel stages. Shared by the kernel and
-// the host (which tells sail_accum_kernel where the staged samples start).
-#ifndef SAIL_GROUP_HOME
-#define SAIL_GROUP_HOME 1
-#endif
-#define SAIL_GROUP_HOME_FOR(kernelSet) (SAIL_GROUP_HOME && (kernelSet) == SAIL_KSET_ROOM)
+// Group home: with sample groups, the room kernel's first group adds its samples to the accumulator itself and the
+// other groups stage theirs (C3 +1 %); in the other kernels the extra path costs more registers than the staged
+// samples it saves (C2 -1.4 %, C4 -0.6 %), so every group stages. Shared by the kernel (traceTileCompact kHome) and the
+// host (which tells sail_accum_kernel where the staged samples start).
+#define SAIL_GROUP_HOME_FOR(kernelSet) ((kernelSet) == SAIL_KSET_ROOM)
 // the exact segment counter is kept as this many partial sums (spread atomics), added on readback
 #define SAIL_SEG_SLOTS 64
 #define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))
@@ -104,18 +101,10 @@ enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
 #define SAIL_KSET_CORNELL_TEX 0u
 #define SAIL_KSET_CORNELL_LIGHTS 0u
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, the UI demo): no quadrics or disks
-#ifndef SAIL_KSET_ROOM_SHAPES
 #define SAIL_KSET_ROOM_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_RECTANGLE) | (1u << SAIL_CORNELLBOX))
-#endif
-#ifndef SAIL_KSET_ROOM_MATS
 #define SAIL_KSET_ROOM_MATS 0xffffffffu
-#endif
-#ifndef SAIL_KSET_ROOM_TEX
 #define SAIL_KSET_ROOM_TEX 0xffffffffu
-#endif
-#ifndef SAIL_KSET_ROOM_LIGHTS
 #define SAIL_KSET_ROOM_LIGHTS 0xffffffffu
-#endif
 
 struct SailFilterArgs {
   const float4* accum;

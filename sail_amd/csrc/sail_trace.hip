@@ -28,43 +28,10 @@
 
 using namespace sm;
 
-#ifndef SAIL_SWEEP_HL
-#define SAIL_SWEEP_HL 1
-#endif
-#ifndef SAIL_SS_UNIT
-#define SAIL_SS_UNIT 1
-#endif
-// SAIL_CULL_LDS_HIT: the pre-cull kernel's hit record reads its winner's row from the LDS copy of the rows (SAIL_CULL_LDS_ROWS);
-// SAIL_CULL_LDS_TP = r: texParams tables of at most r rows are copied into LDS as well (0 = off)
-#ifndef SAIL_CULL_LDS_HIT
-#define SAIL_CULL_LDS_HIT 1
-#endif
-#ifndef SAIL_CULL_LDS_TP
-#define SAIL_CULL_LDS_TP 136
-#endif
-// SAIL_FLAT_LDS = r: the flat compacting kernels copy scenes of at most r rows (and SAIL_FLAT_LDS_TP texParams rows)
-// into LDS for their per-lane hit-record, light-sampler and texParams reads (0 = off; study switch)
-#ifndef SAIL_FLAT_LDS
-#define SAIL_FLAT_LDS 0
-#endif
-#ifndef SAIL_FLAT_LDS_TP
-#define SAIL_FLAT_LDS_TP 16
-#endif
-// SAIL_CULL_LDS_LIGHTS = r: light tables of at most r rows are copied into LDS too (0 = off)
-#ifndef SAIL_CULL_LDS_LIGHTS
-#define SAIL_CULL_LDS_LIGHTS 0
-#endif
-#ifndef SAIL_PRIMS_LDS
-#define SAIL_PRIMS_LDS 0
-#endif
-// one range guard for a ray's three reciprocals; a wave-uniform winner's hit record reads its rows as scalars
-// (measured: C3 +1 %, C4 +4 %, C2 unchanged)
-#ifndef SAIL_RCP3
-#define SAIL_RCP3 1
-#endif
-#ifndef SAIL_HIT_UNIFORM
-#define SAIL_HIT_UNIFORM 1
-#endif
+// Round 4 pruned every measured-and-rejected variant out of this file (their numbers stay in DESIGN.md §6 and
+// profiles/r0*_variants_*.jsonl). What remains is what the four plugin-set kernels run; choices that differ between
+// kernels are compile-time constants of the kernel template (CULL, KS, ...), not build switches. The one build switch
+// left, SAIL_PHASE_TIMING, is instrumentation: tests/test_gpu_parity.py renders through its build too.
 
 #define D __device__ __forceinline__
 
@@ -115,10 +82,7 @@ D V3 localToWorld(V3 v, V3 ns, V3 ss, V3 ts) {
 // their dot products, cross products and frame changes is exact, and each a*b + c rounds once: written fma(a, b, c),
 // bit for bit the unfused sum (the zero-sum sign rule of fma is the addition's; 0 * inf / NaN is NaN either way).
 // Measured bit-identical with ~20 fewer VALU per box-face bounce: C2 -1.2 %, C3 -0.8 % (the second shading-frame
-// branch costs more than it saves there), C4 +0.9 %. 1 = every kernel, 2 (default) = the pre-cull kernel only.
-#ifndef SAIL_AXIS_FRAME
-#define SAIL_AXIS_FRAME 2
-#endif
+// branch costs more than it saves there), C4 +0.9 %: the pre-cull kernel only (Hit.axis).
 D float dotX(V3 a, V3 b) { return fma_(a.z, b.z, fma_(a.y, b.y, a.x * b.x)); }
 D V3 crossX(V3 a, V3 b) {
   return v3(fma_(a.y, b.z, -(a.z * b.y)), fma_(a.z, b.x, -(a.x * b.z)), fma_(a.x, b.y, -(a.y * b.x)));
@@ -130,20 +94,12 @@ D V3 localToWorldX(V3 v, V3 ns, V3 ss, V3 ts) {
 // OBJECT_SPACE_N/S/T (define.glsl:62-64): the full dot products of the reference, so -0 / NaN propagate the same.
 // A product with an exact 0 is exact (a signed zero, or NaN), so "a*0 + b" rounds once either way and is written
 // fma(a, 0, b): bit for bit the same sum (the zero-sum sign rule of fma is the addition's) in fewer instructions.
-#ifndef SAIL_AXIS_FMA
-#define SAIL_AXIS_FMA 1
-#endif
-#if SAIL_AXIS_FMA
 D V3 W2L(V3 v) {  // (dot(v, (0,0,-1)), dot(v, (1,0,0)), dot(v, (0,1,0)))
   return v3(fma_(v.y, 0.0f, v.x * 0.0f) - v.z, fma_(v.z, 0.0f, fma_(v.y, 0.0f, v.x)), fma_(v.z, 0.0f, fma_(v.x, 0.0f, v.y)));
 }
 D V3 L2W(V3 v) {  // (0,0,-1) v.x + (1,0,0) v.y + (0,1,0) v.z, row by row as localToWorld sums them
   return v3(fma_(v.z, 0.0f, fma_(v.x, 0.0f, v.y)), fma_(v.y, 0.0f, v.x * 0.0f) + v.z, fma_(v.z, 0.0f, fma_(v.y, 0.0f, -v.x)));
 }
-#else
-D V3 W2L(V3 v) { return worldToLocal(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
-D V3 L2W(V3 v) { return localToWorld(v, v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)); }
-#endif
 D bool equalZero(float x) { return x < 1e-3f && x > -1e-3f; }
 D float sgn(int rev) { return rev ? -1.0f : 1.0f; }
 
@@ -165,7 +121,6 @@ D bool quadratic(float A, float B, float C, float& t0, float& t1) {  // utility.
 struct Ray { V3 o, d; float rx, ry, rz; };
 D Ray mkRay(V3 o, V3 d) {
   Ray r; r.o = o; r.d = d;
-#if SAIL_RCP3
   // one range guard for the three components (rcp_rn guards each)
   const float mx = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)), mn = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
   if (__builtin_expect(mn >= 0x1p-126f && mx <= 0x1p126f, 1)) {
@@ -176,19 +131,15 @@ D Ray mkRay(V3 o, V3 d) {
   } else {
     r.rx = 1.0f / d.x; r.ry = 1.0f / d.y; r.rz = 1.0f / d.z;
   }
-#else
-  r.rx = rcp_rn(d.x); r.ry = rcp_rn(d.y); r.rz = rcp_rn(d.z);
-#endif
   return r;
 }
-// ---- optional phase timing (tools: -DSAIL_PHASE_TIMING=1 variant builds only): per-wave s_memtime deltas
+// ---- optional phase timing (-DSAIL_PHASE_TIMING=1: libsail_hip_phase.so, tools/phase_profile.py): per-wave
+// s_memtime deltas per phase of the bounce, summed over the launch; the results are those of the plain build
 #ifndef SAIL_PHASE_TIMING
 #define SAIL_PHASE_TIMING 0
 #endif
-#if SAIL_PHASE_TIMING || SAIL_CULL_STATS
-__device__ unsigned long long g_sailPhase[8];
-#endif
 #if SAIL_PHASE_TIMING
+__device__ unsigned long long g_sailPhase[8];
 struct PhaseClock { unsigned long long t, acc[8]; };
 #define PHASE_MARK(pc, k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); (pc).acc[k] += now_ - (pc).t; (pc).t = now_; } while (0)
 #else
@@ -198,12 +149,12 @@ struct PhaseClock {};
 struct Hit {
   float d; V3 hit, normal, dpdu, dpdv; bool into; int matRow; V3 sc, emission; int matCategory;
   float nd;  // dot(geometric normal before the into flip, ray direction)
-  bool axis; // box face: normal / dpdu / dpdv components in {0, +-1} (SAIL_AXIS_FRAME)
+  bool axis; // box face in the pre-cull kernel: normal / dpdu / dpdv components in {0, +-1} (dotX, crossX)
 };
 struct Ctx {
   const float* tp; const float* lt; const int32_t* lightObjRow; const SailPrim* prims;
-  const SailPrim* cprims;  // rows for the candidate loops' per-lane reads: an LDS copy when it fits (SAIL_CULL_LDS_ROWS)
-  const float* tpl;        // texParams rows, an LDS copy when they fit (SAIL_CULL_LDS_TP, SAIL_FLAT_LDS)
+  const SailPrim* cprims;  // rows for the candidate loops' per-lane reads: an LDS copy when it fits (kCullLdsRows)
+  const float* tpl;        // texParams rows, an LDS copy when they fit (kCullLdsTp)
   bool rowCopy, tpCopy;    // per-lane hit-record / light-sampler row reads and texParams reads go through cprims / tpl
   const unsigned long long* typeMasks;
   int n, tn, ln;
@@ -225,11 +176,7 @@ struct Ctx {
 // a wave-uniform primitive read becomes a per-lane vector load (VGPRs + TA cycles) instead of a scalar load.
 template <typename T> using ConstAS = const __attribute__((address_space(4))) T;
 template <typename T> D const T& constRow(const T* base, int i) { return *(const T*)((ConstAS<T>*)base + i); }
-#if SAIL_PRIMS_LDS
-#define PRIM(c, i) ((c).prims[i])
-#else
 #define PRIM(c, i) constRow<SailPrim>((c).prims, (i))
-#endif
 
 D V3 P3(const SailPrim& p, int k) { return v3(p.a[k], p.a[k + 1], p.a[k + 2]); }
 D float TP(const Ctx& c, int row, int col) {
@@ -239,14 +186,7 @@ D float TP(const Ctx& c, int row, int col) {
 D V3 TP3(const Ctx& c, int row, int col) { return v3(TP(c, row, col), TP(c, row, col + 1), TP(c, row, col + 2)); }
 
 // the square root of the warps and BSDF terms whose argument is in [0, 1] by construction (sail_math.h sqrt01)
-#ifndef SAIL_SQRT01
-#define SAIL_SQRT01 1
-#endif
-#if SAIL_SQRT01
 #define SQRT01(x) sqrt01(x)
-#else
-#define SQRT01(x) sqrtf_(x)
-#endif
 // ---- random.glsl:5-18 ---------------------------------------------------------------------------------
 D float hash1(const Ctx& c, float seed, float a, float b, float cc) {
   const V3 p = v3(c.fcx + seed, c.fcy + seed, 0.5f + seed);
@@ -281,12 +221,9 @@ D V2 concentricSampleDisk(V2 u) {
 }
 
 // ---- textures (shader.texture.js:22-29) ----------------------------------------------------------------
-// SAIL_TEX_SHARED: the two checkerboards share uv / size and its floor, so a wave holding both runs them once (same
+// The pre-cull kernel's two checkerboards share uv / size and its floor, so a wave holding both runs them once (same
 // operations). Measured (bit-identical, profiles/r03_variants_tex_shared.jsonl, three rounds): C3 -1.4 %, C4 +0.7 %
-// (its 64 rows mix both textures in most waves): 2 (default) = the pre-cull kernels only, 1 = every kernel, 0 = off.
-#ifndef SAIL_TEX_SHARED
-#define SAIL_TEX_SHARED 2
-#endif
+// (its 64 rows mix both textures in most waves), so the flat kernels keep one branch per texture.
 // UNIFORM_COLOR ignores uv, so hit records skip the UV arithmetic (atan2/acos/divides) for it
 D int matCat(const SailPrim& p) { return (int)(short)(p.cats & 0xffff); }
 D int texCat(const SailPrim& p) { return p.cats >> 16; }
@@ -296,7 +233,7 @@ D V3 getSurfaceColor(const Ctx& c, V2 uv, const SailPrim& p) {
   if (cat == SAIL_TEX_UNIFORM) return TP3(c, texRow, 1);
   if (cat < 0 || cat >= 32 || !((c.texMask >> cat) & 1u)) return v3s(0.0f);
   // c.cullPrims is a compile-time constant in every kernel (the pre-cull ones set 1)
-  if ((SAIL_TEX_SHARED == 1 || (SAIL_TEX_SHARED == 2 && c.cullPrims)) &&
+  if (c.cullPrims &&
       ((cat == SAIL_TEX_CHECKERBOARD && HAS(c.kTex, SAIL_TEX_CHECKERBOARD)) ||
        (cat == SAIL_TEX_CHECKERBOARD2 && HAS(c.kTex, SAIL_TEX_CHECKERBOARD2)))) {
     const bool cb1 = cat == SAIL_TEX_CHECKERBOARD;
@@ -391,19 +328,10 @@ D V3 normalForCornellbox(V3 hit, const SailPrim& p) {  // cornellbox.glsl:39-51
   return v3(0.0f, 0.0f, 1.0f);
 }
 D void dpdBox(V3 normal, V3& dpdu, V3& dpdv) {
-#if SAIL_AXIS_FMA
   const V3 n = normal;  // cross(n, (1,0,0)) / cross(n, (0,1,0)) with the exact zero products folded (see W2L)
   if (fabsf(n.x) < 0.5f) dpdu = v3(fma_(n.y, 0.0f, n.z * -0.0f), fma_(n.x, -0.0f, n.z), fma_(n.x, 0.0f, -n.y));
   else dpdu = v3(fma_(n.y, 0.0f, -n.z), fma_(n.z, 0.0f, n.x * -0.0f), fma_(n.y, -0.0f, n.x));
-#else
-  if (fabsf(normal.x) < 0.5f) dpdu = cross(normal, v3(1.0f, 0.0f, 0.0f));
-  else dpdu = cross(normal, v3(0.0f, 1.0f, 0.0f));
-#endif
-#if SAIL_AXIS_FRAME == 1
-  dpdv = crossX(normal, dpdu);
-#else
   dpdv = cross(normal, dpdu);
-#endif
 }
 D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
   h.hit = r.o + t * r.d;
@@ -424,38 +352,8 @@ D void cubeHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h) {
 // both (z < t excludes z > t; after it the colour test is made as written). Same values, each face test once:
 // 1 = one branch chain, 2 = branch-free selects. Bit-identical but slower (C2 -4.7 % / -3.8 %: more constant moves per
 // branch and more spills), so the default keeps the reference's two chains.
-#ifndef SAIL_CORNELL_ONE_CHAIN
-#define SAIL_CORNELL_ONE_CHAIN 0
-#endif
 D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
   h.hit = r.o + t * r.d;
-#if SAIL_CORNELL_ONE_CHAIN == 2
-  // branch-free: the five face tests once, each face's flag as a lane mask, normal and colour by selects
-  const V3 mn = P3(p, 0), mx = P3(p, 3), x = h.hit;
-  const bool c0 = x.x < mn.x + 0.0001f, c1 = x.x > mx.x - 0.0001f, c2 = x.y < mn.y + 0.0001f,
-             c3 = x.y > mx.y - 0.0001f, c4 = x.z < mn.z + 0.0001f, c5 = x.z > mn.z + 0.0001f;
-  const bool f0 = c0, f1 = !c0 & c1, f2 = !c0 & !c1 & c2, f3 = !c0 & !c1 & !c2 & c3;
-  const bool f4 = !c0 & !c1 & !c2 & !c3 & c4, f5 = !c0 & !c1 & !c2 & !c3 & !c4;
-  const V3 n = v3(f0 ? -1.0f : (f1 ? 1.0f : 0.0f), f2 ? -1.0f : (f3 ? 1.0f : 0.0f), f4 ? -1.0f : (f5 ? 1.0f : 0.0f));
-  const bool white = f2 | f3 | (f5 & c5);  // faces 2, 3 and the lit part of the else face; face 4 is black
-  const float w = white ? 1.0f : 0.0f;
-  const V3 sc = v3((f0 | f1) ? 0.25f : w, f0 ? 0.75f : (f1 ? 0.25f : w), f0 ? 0.25f : (f1 ? 0.75f : w));
-  h.normal = -n;
-  h.sc = sc;
-  dpdBox(h.normal, h.dpdu, h.dpdv);
-#elif SAIL_CORNELL_ONE_CHAIN
-  const V3 mn = P3(p, 0), mx = P3(p, 3), x = h.hit;
-  V3 n, sc;
-  if (x.x < mn.x + 0.0001f) { n = v3(-1.0f, 0.0f, 0.0f); sc = v3(0.25f, 0.75f, 0.25f); }
-  else if (x.x > mx.x - 0.0001f) { n = v3(1.0f, 0.0f, 0.0f); sc = v3(0.25f, 0.25f, 0.75f); }
-  else if (x.y < mn.y + 0.0001f) { n = v3(0.0f, -1.0f, 0.0f); sc = v3s(1.0f); }
-  else if (x.y > mx.y - 0.0001f) { n = v3(0.0f, 1.0f, 0.0f); sc = v3s(1.0f); }
-  else if (x.z < mn.z + 0.0001f) { n = v3(0.0f, 0.0f, -1.0f); sc = v3s(0.0f); }
-  else { n = v3(0.0f, 0.0f, 1.0f); sc = (x.z > mn.z + 0.0001f) ? v3s(1.0f) : v3s(0.0f); }
-  h.normal = -n;
-  h.sc = sc;
-  dpdBox(h.normal, h.dpdu, h.dpdv);
-#else
   h.normal = -normalForCornellbox(r.o + t * r.d, p);
   dpdBox(h.normal, h.dpdu, h.dpdv);
   const V3 mn = P3(p, 0), mx = P3(p, 3), x = h.hit;
@@ -465,21 +363,13 @@ D void cornellHit(const SailPrim& p, const Ray& r, float t, Hit& h) {
   else if (x.y > mx.y - 0.0001f) h.sc = v3s(1.0f);
   else if (x.z > mn.z + 0.0001f) h.sc = v3s(1.0f);
   else h.sc = v3s(0.0f);
-#endif
 }
 
-// SAIL_BOX_UNIFIED: one hit record for both axis-aligned box shapes (a wave holding Cube and Cornellbox lanes, e.g. the
-// README box's ceiling light next to its walls, runs one face chain instead of two). The face chains test the same
-// conditions; the Cube's normal is sgn(rev) * n and the Cornellbox's is -n == -1 * n bit for bit (zeros included);
-// only the surface colour differs (texture vs wall chain).
-// Measured (bit-identical, profiles/r03_variants_box_unified.jsonl): C2 -0.8 %, C3 +0.7 %, C4 +0.1 %; so 2 (default) =
-// the room kernel only, 1 = every kernel, 0 = off.
-#ifndef SAIL_BOX_UNIFIED
-#define SAIL_BOX_UNIFIED 2
-#endif
-// 3 = only in waves whose lanes won different rows (hitRecordU's non-uniform path), 4 = 3 plus every room-kernel wave
-#define SAIL_BOX_UNIFIED_ON(ks) \
-  (SAIL_BOX_UNIFIED == 1 || ((SAIL_BOX_UNIFIED == 2 || SAIL_BOX_UNIFIED == 4) && (ks) == SAIL_KSET_ROOM_SHAPES))
+// The room kernel's one hit record for both axis-aligned box shapes (a wave holding Cube and Cornellbox lanes runs one
+// face chain instead of two). The face chains test the same conditions; the Cube's normal is sgn(rev) * n and the
+// Cornellbox's is -n == -1 * n bit for bit (zeros included); only the surface colour differs (texture vs wall chain).
+// Measured (bit-identical, profiles/r03_variants_box_unified*.jsonl): room kernel C3 +0.7 %; every kernel C2 -0.8 %,
+// C4 +0.1 %; only in mixed waves C2 +-0.2 %, C3 -0.7 %, so the room kernel alone takes it.
 D void boxHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h, bool cornell) {
   h.hit = r.o + t * r.d;
   const float s = cornell ? -1.0f : sgn(p.rev);
@@ -508,16 +398,10 @@ D void boxHit(const Ctx& c, const SailPrim& p, const Ray& r, float t, Hit& h, bo
 // The quadrics' bounding-box test (testBoundboxFor*) and their root search are both pure predicates on the
 // ray, so their order is free: the discriminant rejects most rays more cheaply than the six-divide slab test,
 // and only candidate hits pay the exact slab test (same results; C3 +4 %, C4 +5 %, measured).
-#ifndef SAIL_BOX_LAST
-#define SAIL_BOX_LAST 1
-#endif
 // ---- sphere.glsl:45-86 ---------------------------------------------------------------------------------------
 D float sphereT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 c = P3(p, 0);
   const float rad = p.a[3];
-#if !SAIL_BOX_LAST
-  if (!testBoundbox(r0, c - v3s(rad), c + v3s(rad))) return kMaxDistance;
-#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - c);
   const float a = dot(d, d), b = 2.0f * dot(o, d), cc = dot(o, o) - rad * rad;
   float t1 = 0.0f, t2 = 0.0f;
@@ -526,9 +410,7 @@ D float sphereT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   float t = t1;
   if (t1 < kEps) t = t2;
   if (t >= kMaxDistance) return kMaxDistance;
-#if SAIL_BOX_LAST
   if (!testBoundbox(r0, c - v3s(rad), c + v3s(rad))) return kMaxDistance;
-#endif
   if (hitOut) *hitOut = o + t * d;
   return t;
 }
@@ -540,18 +422,10 @@ D float phiOf(float y, float x) {
 D V3 dpduRot(V3 hit) { return v3(-2.0f * kPI * hit.y, 2.0f * kPI * hit.x, 0.0f); }
 // cross(a, b) with a.z == 0 (crossZa) or b.z == 0 (crossZb), the exact zero products folded as in W2L
 D V3 crossZa(V3 a, V3 b) {
-#if SAIL_AXIS_FMA
   return v3(fma_(b.y, -0.0f, a.y * b.z), fma_(b.x, 0.0f, -(a.x * b.z)), a.x * b.y - a.y * b.x);
-#else
-  return cross(a, b);
-#endif
 }
 D V3 crossZb(V3 a, V3 b) {
-#if SAIL_AXIS_FMA
   return v3(fma_(a.y, 0.0f, -(a.z * b.y)), fma_(a.x, -0.0f, a.z * b.x), a.x * b.y - a.y * b.x);
-#else
-  return cross(a, b);
-#endif
 }
 D void sphereHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const float rad = p.a[3];
@@ -626,9 +500,6 @@ D bool rootPick(float t1, float t2, V3 o, V3 d, float zlo, float zhi, bool epsLo
 D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float h = p.a[3], rad = p.a[4];
-#if !SAIL_BOX_LAST
-  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
-#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float k = p.a[5];  // (rad / h)^2, per scene
   const float a = d.x * d.x + d.y * d.y - k * d.z * d.z;
@@ -638,18 +509,13 @@ D float coneT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
-#if SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
-#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
 D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float h = p.a[3], rad = p.a[4];
-#if !SAIL_BOX_LAST
-  if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
-#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float a = d.x * d.x + d.y * d.y;
   const float b = 2.0f * (d.x * o.x + d.y * o.y);
@@ -658,21 +524,13 @@ D float cylinderT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, 0.0f, h, true, t, hit)) return kMaxDistance;
-#if SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, 0.0f, rad), pp + v3(rad, h, rad))) return kMaxDistance;
-#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
 D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float ah = p.a[9], ch = p.a[10];
-#if !SAIL_BOX_LAST
-  {  // testBoundboxForHyperboloid :13-24 (rMax, zMin, zMax per scene)
-    const float rMax = p.a[11], zMin = p.a[12], zMax = p.a[13];
-    if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
-  }
-#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float a = ah * d.x * d.x + ah * d.y * d.y - ch * d.z * d.z;
   const float b = 2.0f * (ah * d.x * o.x + ah * d.y * o.y - ch * d.z * o.z);
@@ -682,12 +540,10 @@ D float hypT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (t2 < -kEps) return kMaxDistance;
   const float zMin = p.a[12], zMax = p.a[13];
   if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
-#if SAIL_BOX_LAST
   {  // testBoundboxForHyperboloid :13-24 (rMax, zMin, zMax per scene)
     const float rMax = p.a[11], zMin = p.a[12], zMax = p.a[13];
     if (!testBoundbox(r0, pp - v3(rMax, -zMin, rMax), pp + v3(rMax, zMax, rMax))) return kMaxDistance;
   }
-#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
@@ -695,9 +551,6 @@ D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const V3 pp = P3(p, 0);
   const float z0 = p.a[3], z1 = p.a[4], rad = p.a[5];
   const float zMin = fmin_(z0, z1), zMax = fmax_(z0, z1);
-#if !SAIL_BOX_LAST
-  if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
-#endif
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   const float k = p.a[6];  // zMax / (rad * rad), per scene
   const float a = k * (d.x * d.x + d.y * d.y);
@@ -707,9 +560,7 @@ D float paraT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   if (!quadratic(a, b, cc, t1, t2)) return kMaxDistance;
   if (t2 < -kEps) return kMaxDistance;
   if (!rootPick(t1, t2, o, d, zMin, zMax, false, t, hit)) return kMaxDistance;
-#if SAIL_BOX_LAST
   if (!testBoundbox(r0, pp - v3(rad, -zMin, rad), pp + v3(rad, zMax, rad))) return kMaxDistance;
-#endif
   if (hitOut) *hitOut = hit;
   return t;
 }
@@ -727,51 +578,20 @@ D float diskT(const SailPrim& p, const Ray& r0, V3* hitOut) {  // disk.glsl:36-7
   if (hitOut) *hitOut = hit;
   return t;
 }
-// SAIL_QUAD_SHARED: the pre-cull kernel's candidate sweep tests cones, cylinders, hyperboloids and paraboloids in one
+// The pre-cull kernel's candidate sweep tests cones, cylinders, hyperboloids and paraboloids in one
 // loop (quadT) instead of one loop per type. A wave then runs max-over-lanes(quadric candidates) iterations instead
 // of the sum over the four types of max-over-lanes(candidates of the type). Per type only the coefficients and the
 // z-range / box parameters differ; the ray transform, the root solve, rootPick and the box test are shared. Same
-// operations on the same values as coneT / cylinderT / hypT / paraT (box test last, SAIL_BOX_LAST). Candidates are
-// visited out of row order either way (the take rule keeps the in-order winner).
-// Measured (bit-identical, profiles/r03_variants_quad_shared.jsonl, three rounds): C4 +0.9 %. 1 (default) = the four
-// quadrics, 2 = the sphere too (its own root rule), 3 = the disk too (planar), 0 = one loop per type.
-#ifndef SAIL_QUAD_SHARED
-#define SAIL_QUAD_SHARED 1
-#endif
-D bool isQuadric(int t) {
-  return t == SAIL_CONE || t == SAIL_CYLINDER || t == SAIL_HYPERBOLOID || t == SAIL_PARABOLOID;
-}
+// operations on the same values as coneT / cylinderT / hypT / paraT (box test last). Candidates are visited out of
+// row order either way (the take rule keeps the in-order winner).
+// Measured (bit-identical, profiles/r03_variants_quad_shared.jsonl, three rounds): C4 +0.9 %; with the sphere in the
+// same loop (its own root rule) -5.4 %, with the planar disk -0.6 %.
 D float quadT(const SailPrim& p, const Ray& r0, V3* hitOut) {
   const int ty = p.type;
   const V3 pp = P3(p, 0);
   const V3 d = W2L(r0.d), o = W2L(r0.o - pp);
   float a, b, cc, zlo, zhi, bA, bB, bC;
   bool epsLo;
-  if (SAIL_QUAD_SHARED == 3 && ty == SAIL_DISK) {  // diskT (disk.glsl:36-75)
-    const float rad = p.a[3], ri = p.a[4];
-    if (d.z == 0.0f) return kMaxDistance;
-    const float t = fdiv(-o.z, d.z);
-    if (t <= 0.0f) return kMaxDistance;
-    const V3 hit = o + t * d;
-    const float dist2 = hit.x * hit.x + hit.y * hit.y;
-    if (dist2 > rad * rad || dist2 < ri * ri) return kMaxDistance;
-    if (t >= kMaxDistance) return kMaxDistance;
-    if (hitOut) *hitOut = hit;
-    return t;
-  }
-  if (SAIL_QUAD_SHARED == 2 && ty == SAIL_SPHERE) {  // sphereT (sphere.glsl:45-86)
-    const float rad = p.a[3];
-    const float sa = dot(d, d), sb = 2.0f * dot(o, d), sc = dot(o, o) - rad * rad;
-    float t1 = 0.0f, t2 = 0.0f;
-    if (!quadratic(sa, sb, sc, t1, t2)) return kMaxDistance;
-    if (t2 < kEps) return kMaxDistance;
-    float t = t1;
-    if (t1 < kEps) t = t2;
-    if (t >= kMaxDistance) return kMaxDistance;
-    if (!testBoundbox(r0, pp - v3s(rad), pp + v3s(rad))) return kMaxDistance;
-    if (hitOut) *hitOut = o + t * d;
-    return t;
-  }
   if (ty == SAIL_CONE) {
     const float h = p.a[3], rad = p.a[4], k = p.a[5];
     a = d.x * d.x + d.y * d.y - k * d.z * d.z;
@@ -867,21 +687,13 @@ D void diskHit(const Ctx& c, const SailPrim& p, V3 hit, Hit& h) {
   const V3 dpdv = v3(hit.x, hit.y, 0.0f) * (ri - rad) / sqrtf_(dist2);
   finishLocal(c, p, hit, uv, dpduRot(hit), dpdv, h);
 }
-// SAIL_LOCAL_SHARED: one hit record for the six local-space shapes (sphere, cone, cylinder, hyperboloid, paraboloid,
+// localHit, the pre-cull kernel's one hit record for the six local-space shapes (sphere, cone, cylinder, hyperboloid, paraboloid,
 // disk). Each computes the same tail -- the azimuth phiOf (atan2) of its UV, dpdu = dpduRot(hit), a normalised cross,
 // the texture and four local-to-world transforms -- so a wave whose lanes hit different shape types (the pre-cull
 // kernel sorts by material, then shape) runs that tail once instead of once per type. Per type only the phi
 // arguments, the v coordinate, dpdv and the cross order differ. Same operations on the same values as sphereHit and
-// the finishLocal callers above. 1 = every kernel, 2 = the pre-cull kernels, 3 = the pre-cull kernels' waves whose
-// lanes won different rows, 0 = off. Measured (bit-identical, profiles/r03_variants_local_shared.jsonl, three rounds):
-// 2 C4 +3.3 %, C2/C3 unchanged; 3 C4 +3.2 %; 1 C4 +3.1 %, C3 -0.8 %. Default 2.
-#ifndef SAIL_LOCAL_SHARED
-#define SAIL_LOCAL_SHARED 2
-#endif
-D bool isLocalShape(int t) {
-  return t == SAIL_SPHERE || t == SAIL_CONE || t == SAIL_CYLINDER || t == SAIL_HYPERBOLOID || t == SAIL_PARABOLOID ||
-         t == SAIL_DISK;
-}
+// the finishLocal callers above. Measured (bit-identical, profiles/r03_variants_local_shared.jsonl, three rounds):
+// pre-cull kernel C4 +3.3 %, C2/C3 unchanged; only its mixed waves +3.2 %; every kernel C4 +3.1 %, C3 -0.8 %.
 D void localHit(const Ctx& c, const SailPrim& p, V3 hl, Hit& h) {
   const int ty = p.type;
   const bool nUV = needsUV(p);
@@ -985,46 +797,16 @@ D float primT(const Ctx& c, const SailPrim& p, const Ray& r, V3* hl) {
 // Cheap conservative pre-cull: the ray against the primitive's padded bounds in f32 (sail_capi.cpp
 // padPrimBounds). It rejects only rays that miss the padded box or enter it beyond the closest distance so
 // far (with margin); such a primitive's exact test could only return a miss or a larger distance.
-#if SAIL_CULL_PK
-typedef float sf2 __attribute__((ext_vector_type(2)));
-#endif
 D bool padHit(const SailPrim& p, const Ray& r, float best) {
-#if SAIL_CULL_PK
-  // the x and y slabs as packed pairs (v_pk_add_f32 / v_pk_mul_f32): the same IEEE operations, half the issues
-  const sf2 oxy = {r.o.x, r.o.y}, rxy = {r.rx, r.ry};
-  const sf2 lo = (sf2{p.a[18], p.a[19]} - oxy) * rxy, hi = (sf2{p.a[21], p.a[22]} - oxy) * rxy;
-  const float x0 = lo.x, x1 = hi.x, y0 = lo.y, y1 = hi.y;
-  const float z0 = (p.a[20] - r.o.z) * r.rz, z1 = (p.a[23] - r.o.z) * r.rz;
-#else
   const float ix = r.rx, iy = r.ry, iz = r.rz;
   const float x0 = (p.a[18] - r.o.x) * ix, x1 = (p.a[21] - r.o.x) * ix;
   const float y0 = (p.a[19] - r.o.y) * iy, y1 = (p.a[22] - r.o.y) * iy;
   const float z0 = (p.a[20] - r.o.z) * iz, z1 = (p.a[23] - r.o.z) * iz;
-#endif
   const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
   const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
   return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > best * 1.0001f + 1e-4f);
 }
 
-// -DSAIL_CULL_STATS=1 (variant builds only): per (wave, primitive) counts of pre-cull outcomes in g_sailPhase:
-// [0] tests, [1] tests where some lane passed, [2] passing lanes, [3] active lanes
-#ifndef SAIL_CULL_STATS
-#define SAIL_CULL_STATS 0
-#endif
-#if SAIL_CULL_STATS
-D void cullStat(bool pass) {
-  const unsigned long long act = __ballot(1), m = __ballot(pass);
-  if (__lane_id() == (unsigned)(__ffsll((long long)act) - 1)) {
-    atomicAdd(&g_sailPhase[0], 1ull);
-    if (m) atomicAdd(&g_sailPhase[1], 1ull);
-    atomicAdd(&g_sailPhase[2], (unsigned long long)__popcll(m));
-    atomicAdd(&g_sailPhase[3], (unsigned long long)__popcll(act));
-  }
-}
-#define CULL_TEST(c, p, r, best) ([&]() { const bool ok_ = padHit(p, r, best); cullStat(ok_); return ok_; }())
-#else
-#define CULL_TEST(c, p, r, best) padHit(p, r, best)
-#endif
 
 // ---- candidate sweep (pre-cull kernel) ----------------------------------------------------------------------
 // In the uniform sweep a wave runs a primitive's exact test whenever any lane passes its pre-cull; on C4
@@ -1034,20 +816,11 @@ D void cullStat(bool pass) {
 // type: the wave runs max-over-lanes iterations instead of one per primitive any lane needs. Candidates are
 // visited out of row order, so a hit replaces the best one when it is nearer, or equally near with a lower
 // row -- the winner of the in-order "t < best" sweep. Pre-culled rows cannot win (padHit), nor tie.
-#ifndef SAIL_CAND_SWEEP
-#define SAIL_CAND_SWEEP 1
-#endif
-#ifndef SAIL_CAND_RECULL
-#define SAIL_CAND_RECULL 0
-#endif
-// SAIL_CAND_FLAT=1: candidate loops without exec-mask nesting (idle lanes test a real row of the type, `take`
-// keeps them out): bit-identical, C4 -0.8 % (the idle lanes' own branches cost more than the saved masking)
-#ifndef SAIL_CAND_FLAT
-#define SAIL_CAND_FLAT 0
-#endif
+// Candidate loops without exec-mask nesting (idle lanes test a real row of the type, `take` keeps them out) were
+// bit-identical and C4 -0.8 % (the idle lanes' own branches cost more than the saved masking).
 // candidate masks built from descending rows shifted into two 32-bit halves (one select + one v_lshl_or per
 // row instead of a 64-bit shift, two moves, two selects and two ors): C4 +2.7 %. Packing the x/y slab
-// arithmetic of padHit into v_pk_add_f32 / v_pk_mul_f32 (SAIL_CULL_PK) was measured at -3.4 %.
+// arithmetic of padHit into v_pk_add_f32 / v_pk_mul_f32 was measured at -3.4 %.
 // Fused pre-cull form (A.cullPrims == 2): each slab plane as fma(a, R, -RN(o R)), 2 FMAs per axis instead of
 // 2 subtractions + 2 multiplies, o R hoisted per ray. Against the plain form each plane moves by at most
 // |o| 2^-24 (the host enables it only while that is far inside the padding: sail_capi.cpp cullFmaOk). The
@@ -1062,24 +835,12 @@ D CullRay cullRay(const Ray& r) {
   q.ox = -(r.o.x * q.rx); q.oy = -(r.o.y * q.ry); q.oz = -(r.o.z * q.rz);
   return q;
 }
-// B = best * 1.0001 + 1e-4 (> 0), computed once per chunk by the caller
-D bool padHitF(const SailPrim& p, const CullRay& q, float B) {
-  const float x0 = fma_(p.a[18], q.rx, q.ox), x1 = fma_(p.a[21], q.rx, q.ox);
-  const float y0 = fma_(p.a[19], q.ry, q.oy), y1 = fma_(p.a[22], q.ry, q.oy);
-  const float z0 = fma_(p.a[20], q.rz, q.oz), z1 = fma_(p.a[23], q.rz, q.oz);
-  const float tmin = fmax_(fmax_(fmin_(x0, x1), fmin_(y0, y1)), fmin_(z0, z1));
-  const float tmax = fmin_(fmin_(fmax_(x0, x1), fmax_(y0, y1)), fmax_(z0, z1));
-  return !(tmin > tmax) && !(tmax < 0.0f) && !(tmin > B);
-}
-// Mask build with the row's outcome as the compare's own lane mask (SAIL_MASK_ASM, fused form only): the bit is
+// Mask build in the fused form, B = best * 1.0001 + 1e-4 (> 0) computed once per chunk by the caller. The row's
+// outcome is the compare's own lane mask: the bit is
 // shifted in by one v_addc (v + v + carry, the carry-in being that lane mask) instead of a select and a v_lshl_or,
 // and min(tmax, B) is one v_min_f32 -- the compiler's own fold of the three tests, which re-canonicalised the
 // loop-invariant B on every row (tmax and B are arithmetic results, never signalling NaNs, so the plain hardware
 // min is the same value). Two fewer VALU per row of the ~20 of each pre-cull test.
-#ifndef SAIL_MASK_ASM
-#define SAIL_MASK_ASM 1
-#endif
-#if SAIL_MASK_ASM
 D unsigned long long padHitFMask(const SailPrim& p, const CullRay& q, float B) {
   const float x0 = fma_(p.a[18], q.rx, q.ox), x1 = fma_(p.a[21], q.rx, q.ox);
   const float y0 = fma_(p.a[19], q.ry, q.oy), y1 = fma_(p.a[22], q.ry, q.oy);
@@ -1097,24 +858,19 @@ D unsigned shiftInMask(unsigned v, unsigned long long laneMask) {
   __asm__("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carryOut) : "v"(v), "s"(laneMask));
   return r;
 }
-#endif
-// one 64-row chunk's candidate mask: descending rows shifted into two 32-bit halves (one select and one
-// v_lshl_or per row; one v_addc with SAIL_MASK_ASM)
+// one 64-row chunk's candidate mask: descending rows shifted into two 32-bit halves (one v_addc per row in the fused
+// form; one select and one v_lshl_or per row in the plain one)
 template <bool FUSED>
 D unsigned long long chunkMask(const Ctx& c, const Ray& r, const CullRay& q, int base, int cnt, float bound) {
   unsigned lo = 0u, hi = 0u;
   const float B = bound * 1.0001f + 1e-4f;
-#if SAIL_MASK_ASM
   if (FUSED) {
     for (int j = cnt - 1; j >= 32; j--) hi = shiftInMask(hi, padHitFMask(PRIM(c, base + j), q, B));
     for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = shiftInMask(lo, padHitFMask(PRIM(c, base + j), q, B));
     return ((unsigned long long)hi << 32) | lo;
   }
-#endif
-#define SWEEP_TEST(j) (FUSED ? padHitF(PRIM(c, base + (j)), q, B) : CULL_TEST(c, PRIM(c, base + (j)), r, bound))
-  for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (SWEEP_TEST(j) ? 1u : 0u);
-  for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = (lo << 1) | (SWEEP_TEST(j) ? 1u : 0u);
-#undef SWEEP_TEST
+  for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (padHit(PRIM(c, base + j), r, bound) ? 1u : 0u);
+  for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = (lo << 1) | (padHit(PRIM(c, base + j), r, bound) ? 1u : 0u);
   return ((unsigned long long)hi << 32) | lo;
 }
 template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
@@ -1133,42 +889,17 @@ template <int T> D float typedT(const SailPrim& p, const Ray& r, V3* hl) {
 // is kept, and an equally near candidate changes nothing (a tie leaves the distance's value as it is; +-0 compare
 // equal and both fail the caller's d > EPSILON). Four fewer live registers in the shadow sweep, where the
 // shading state is live.
-#ifndef SAIL_SHADOW_T_ONLY
-#define SAIL_SHADOW_T_ONLY 1
-#endif
 template <int T, bool HIT>
 D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
   if (!HAS(c.kShapes, T)) return;
   const unsigned long long tm = constRow<unsigned long long>(c.typeMasks, (base >> 6) * 16 + T);
   unsigned long long m = cand & tm;
-#if SAIL_CAND_FLAT
-  // every lane of the wave runs each iteration: a lane whose candidates of this type are used up tests the
-  // chunk's first row of type T (a real primitive of the same shape, so its branches stay those of a typical
-  // lane) and keeps its result out by `take`. No exec-mask nesting around the test, so the loop-carried winner
-  // needs no copies at every iteration.
-  while (__builtin_amdgcn_ballot_w64(m != 0ull)) {
-    const bool has = m != 0ull;
-    const int i = base + __builtin_ctzll(has ? m : tm);
-    m &= m - 1ull;  // 0 stays 0
-    const SailPrim& p = c.cprims[i];
-    V3 hl = v3s(0.0f);
-    const float t = typedT<T>(p, r, &hl);
-    const bool take = has & ((t < best) | ((t == best) & (i < bi)));
-    best = take ? t : best;
-    bi = take ? i : bi;
-    bhl.x = take ? hl.x : bhl.x; bhl.y = take ? hl.y : bhl.y; bhl.z = take ? hl.z : bhl.z;
-  }
-  return;
-#endif
   while (__ballot(m != 0ull)) {
     if (m != 0ull) {
       const int i = base + __builtin_ctzll(m);
       m &= m - 1ull;
       const SailPrim& p = c.cprims[i];
-#if SAIL_CAND_RECULL
-      if (!padHit(p, r, best)) continue;
-#endif
-      if (HIT || !SAIL_SHADOW_T_ONLY) {
+      if (HIT) {
         V3 hl = v3s(0.0f);
         const float t = typedT<T>(p, r, &hl);
         if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
@@ -1179,12 +910,11 @@ D void candType(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
     }
   }
 }
-// the four quadric types' candidates in one loop (SAIL_QUAD_SHARED)
+// the four quadric types' candidates in one loop (quadT)
 template <bool HIT>
 D void candQuad(const Ctx& c, const Ray& r, int base, unsigned long long cand, float& best, int& bi, V3& bhl) {
   const uint32_t kq = c.kShapes & ((1u << SAIL_CONE) | (1u << SAIL_CYLINDER) | (1u << SAIL_HYPERBOLOID) |
-                                   (1u << SAIL_PARABOLOID) | (SAIL_QUAD_SHARED == 2 ? (1u << SAIL_SPHERE) : 0u) |
-                                   (SAIL_QUAD_SHARED == 3 ? (1u << SAIL_DISK) : 0u));
+                                   (1u << SAIL_PARABOLOID));
   if (kq == 0u) return;
   const unsigned long long* tms = c.typeMasks + (base >> 6) * 16;
   unsigned long long tm = 0ull;
@@ -1192,15 +922,13 @@ D void candQuad(const Ctx& c, const Ray& r, int base, unsigned long long cand, f
   if (HAS(kq, SAIL_CYLINDER)) tm |= constRow<unsigned long long>(tms, SAIL_CYLINDER);
   if (HAS(kq, SAIL_HYPERBOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_HYPERBOLOID);
   if (HAS(kq, SAIL_PARABOLOID)) tm |= constRow<unsigned long long>(tms, SAIL_PARABOLOID);
-  if (HAS(kq, SAIL_SPHERE)) tm |= constRow<unsigned long long>(tms, SAIL_SPHERE);
-  if (HAS(kq, SAIL_DISK)) tm |= constRow<unsigned long long>(tms, SAIL_DISK);
   unsigned long long m = cand & tm;
   while (__ballot(m != 0ull)) {
     if (m != 0ull) {
       const int i = base + __builtin_ctzll(m);
       m &= m - 1ull;
       const SailPrim& p = c.cprims[i];
-      if (HIT || !SAIL_SHADOW_T_ONLY) {
+      if (HIT) {
         V3 hl = v3s(0.0f);
         const float t = quadT(p, r, &hl);
         if (t < best || (t == best && i < bi)) { best = t; bi = i; bhl = hl; }
@@ -1223,20 +951,9 @@ D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, 
     candType<SAIL_CUBE, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_CORNELLBOX, HIT>(c, r, base, cand, best, bi, bhl);
     candType<SAIL_RECTANGLE, HIT>(c, r, base, cand, best, bi, bhl);
-#if !(SAIL_QUAD_SHARED == 3 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
     candType<SAIL_DISK, HIT>(c, r, base, cand, best, bi, bhl);
-#endif
-#if !(SAIL_QUAD_SHARED == 2 && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL)
     candType<SAIL_SPHERE, HIT>(c, r, base, cand, best, bi, bhl);
-#endif
-#if SAIL_QUAD_SHARED && SAIL_BOX_LAST && !SAIL_CAND_FLAT && !SAIL_CAND_RECULL
     candQuad<HIT>(c, r, base, cand, best, bi, bhl);
-#else
-    candType<SAIL_CYLINDER, HIT>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_CONE, HIT>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_PARABOLOID, HIT>(c, r, base, cand, best, bi, bhl);
-    candType<SAIL_HYPERBOLOID, HIT>(c, r, base, cand, best, bi, bhl);
-#endif
   }
 }
 
@@ -1246,15 +963,13 @@ D void candSweep(const Ctx& c, const Ray& r, float limit, float& best, int& bi, 
 // starts at 1 instead of MAX_DISTANCE. Returned distances beyond that bound are not exact.
 D float closestT(const Ctx& c, const Ray& r) {
   float best = kMaxDistance;
-#if SAIL_CAND_SWEEP
   if (c.cullPrims && !c.shadowAnyHit) {
     int bi = -1; V3 bhl = v3s(0.0f);
     candSweep<false>(c, r, 1.0f, best, bi, bhl);
     return best;
   }
-#endif
   for (int i = 0; i < c.n; i++) {
-    if (c.cullPrims && !CULL_TEST(c, PRIM(c, i), r, fmin_(best, 1.0f))) continue;
+    if (c.cullPrims && !padHit(PRIM(c, i), r, fmin_(best, 1.0f))) continue;
     const float t = primT(c, PRIM(c, i), r, nullptr);
     if (t < best) {
       best = t;
@@ -1273,34 +988,23 @@ D Sweep sweepRay(const Ctx& c, const Ray& r, bool primary) {
   int bi = -1;
   V3 bhl = v3s(0.0f);
   const bool cull = c.cullPrims && (!primary || c.cullPrimary);
-#if SAIL_CAND_SWEEP
   if (cull) {
     candSweep<true>(c, r, kMaxDistance, best, bi, bhl);
     Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
     return sw;
   }
-#endif
-#if SAIL_SWEEP_HL
   for (int i = 0; i < c.n; i++) {
-    if (cull && !CULL_TEST(c, PRIM(c, i), r, best)) continue;
     V3 hl = v3s(0.0f);
     const float t = primT(c, PRIM(c, i), r, &hl);
     if (t < best) { best = t; bi = i; bhl = hl; }
   }
-#else
-  for (int i = 0; i < c.n; i++) {
-    const float t = primT(c, PRIM(c, i), r, nullptr);
-    if (t < best) { best = t; bi = i; }
-  }
-  if (bi >= 0) primT(c, PRIM(c, bi), r, &bhl);  // the same arithmetic again, for the winner only
-#endif
   Sweep sw; sw.best = best; sw.bi = bi; sw.bhl = bhl;
   return sw;
 }
 // The winner's local hit point from the ray and its distance: every local-space intersect above ends with
 // hit = o + t * d on the same local o and d (W2L of the ray for the quadrics and the disk, the rectangle's frame), so
 // this is the sweep's own value bit for bit -- the compacting kernels recompute it instead of moving it through LDS
-// (SAIL_STATE_PACK).
+// (packed path state, traceTileCompact).
 D V3 quadLocalHit(const SailPrim& p, const Ray& r, float t) {
   const V3 d = W2L(r.d), o = W2L(r.o - P3(p, 0));
   return o + t * d;
@@ -1311,8 +1015,7 @@ D V3 rectLocalHit(const SailPrim& p, const Ray& r, float t) {
   const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
   return o + t * d;
 }
-// MIXED: the record of a wave whose lanes won different rows (hitRecordU), where SAIL_BOX_UNIFIED 3 / 4 share the box code
-template <bool RECOMP_HL = false, bool MIXED = false>
+template <bool RECOMP_HL = false>
 D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const float best = sw.best;
   const int bi = sw.bi;
@@ -1323,9 +1026,10 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   // zero default would be materialised for every lane before the dispatch
   const SailPrim& p = c.rowCopy ? c.cprims[bi] : PRIM(c, bi);
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
-  const bool boxU = SAIL_BOX_UNIFIED_ON(c.kShapes) || (SAIL_BOX_UNIFIED >= 3 && MIXED);  // compile-time constant
-  const bool localU = SAIL_LOCAL_SHARED == 1 || (SAIL_LOCAL_SHARED == 2 && c.cullPrims) ||
-                      (SAIL_LOCAL_SHARED == 3 && c.cullPrims && MIXED);
+  // compile-time constants: the room kernel's shared box record (boxHit), the pre-cull kernel's shared local-space
+  // record (localHit)
+  const bool boxU = c.kShapes == SAIL_KSET_ROOM_SHAPES;
+  const bool localU = c.cullPrims != 0;
   const uint32_t kLocal = c.kShapes & ((1u << SAIL_SPHERE) | (1u << SAIL_CONE) | (1u << SAIL_CYLINDER) |
                                        (1u << SAIL_HYPERBOLOID) | (1u << SAIL_PARABOLOID) | (1u << SAIL_DISK));
   if (boxU && ((HAS(c.kShapes, SAIL_CUBE) && p.type == SAIL_CUBE) ||
@@ -1351,12 +1055,8 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   h.emission = v3(p.em[0], p.em[1], p.em[2]);
   // faceObj test (shader.shape.js:47-49) on sgn(rev) * normal: (-n).d is exactly -(n.d) (negated products,
   // round-to-nearest is symmetric), so one dot product serves it and the into test below
-#if SAIL_AXIS_FRAME
-  h.axis = (SAIL_AXIS_FRAME == 1 || c.cullPrims) && (p.type == SAIL_CUBE || p.type == SAIL_CORNELLBOX);
+  h.axis = c.cullPrims && (p.type == SAIL_CUBE || p.type == SAIL_CORNELLBOX);
   const float nd = h.axis ? dotX(h.normal, r.d) : dot(h.normal, r.d);
-#else
-  const float nd = dot(h.normal, r.d);
-#endif
   if (!((p.rev ? -nd : nd) < -kEps)) h.emission = v3s(0.0f);
   h.matCategory = matCat(p);
   h.into = nd < -kEps;
@@ -1367,39 +1067,24 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
 // wave-uniform winner: the same record with the row index in an SGPR (scalar row loads)
 template <bool RECOMP_HL = false>
 D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
-#if SAIL_HIT_UNIFORM
   const int b0 = __builtin_amdgcn_readfirstlane(sw.bi);
   if (__all(sw.bi == b0)) {
     Sweep su = sw;
     su.bi = b0;
     return hitRecord<RECOMP_HL>(c, r, su);
   }
-#endif
-  return hitRecord<RECOMP_HL, true>(c, r, sw);
-}
-D Hit intersectObjects(const Ctx& c, const Ray& r, bool primary, PhaseClock& pc) {
-  const Sweep sw = sweepRay(c, r, primary);
-  PHASE_MARK(pc, 0);  // primitive sweep
-  if (sw.bi < 0) {  // a miss: only d is read (the AOV store substitutes zeros)
-    Hit h;
-    h.d = sw.best;
-    h.hit = v3s(0.0f); h.normal = v3s(0.0f); h.dpdu = v3s(0.0f); h.dpdv = v3s(0.0f);
-    h.sc = v3s(0.0f); h.emission = v3s(0.0f); h.matRow = 0; h.into = false; h.matCategory = 0; h.nd = 0.0f; h.axis = false;
-    return h;
-  }
-  return hitRecord(c, r, sw);
+  return hitRecord<RECOMP_HL>(c, r, sw);
 }
 
 // ---- sampleGeometry for area lights (shader.shape.js:53-67) -----------------------------------------------------
-// qs (may be null): uniformSampleSphere(u), already computed by the caller (SAIL_LIGHT_SHARED)
-D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf, const V3* qs = nullptr) {
+D V3 sampleGeometry(const Ctx& c, V2 u, int row, V3& normal, float& pdf) {
   normal = v3s(0.0f);
   pdf = 0.0f;
   const SailPrim& p = c.rowCopy ? c.cprims[row] : PRIM(c, row);
   const float s = sgn(p.rev);
   switch (p.type) {
     case SAIL_SPHERE: if (!HAS(c.kShapes, SAIL_SPHERE)) break; {
-      const V3 q = qs ? *qs : uniformSampleSphere(u);
+      const V3 q = uniformSampleSphere(u);
       const float rad = p.a[3];
       pdf = fdiv(kInvPI, rad * rad);
       const V3 res = q * rad + P3(p, 0);
@@ -1669,11 +1354,8 @@ D V3 material(const Ctx& c, const Hit& ins, V2 u, V3 wo, V3& wi, V3& f) {
 }
 
 // ---- lights (shader.light.js:12-22, light/*.glsl) ---------------------------------------------------------------
-// study switch (bit-identical, profiles/r03_variants_light_shared.jsonl): C4 -0.35 % -- the extra light-row read and the
-// hoisted sample cost more than the second evaluation it saves -- so 0 (off)
-#ifndef SAIL_LIGHT_SHARED
-#define SAIL_LIGHT_SHARED 0
-#endif
+// (one uniformSampleSphere shared by point lights and sphere area lights was bit-identical and C4 -0.35 %,
+// profiles/r03_variants_light_shared.jsonl: the extra light-row read cost more than the second evaluation)
 D bool testShadow(const Ctx& c, const Ray& r) {
   const float d = closestT(c, r);
   return d > kEps && d < kOneMinusEps;
@@ -1699,26 +1381,17 @@ D LightPrep lightPrep(const Ctx& c, const Hit& ins, V2 u2) {
   const float* L = c.lt + row * 18;
   V3 contrib = v3s(0.0f), toLight = v3s(0.0f);
   bool lit = false;
-  // SAIL_LIGHT_SHARED (pre-cull kernels): the sphere direction sample of a point light and of a sphere area light is
-  // the same uniformSampleSphere(u2), evaluated once for the wave's lanes of both kinds
-  const bool lshared = SAIL_LIGHT_SHARED && c.cullPrims && HAS(c.kLights, SAIL_POINT) && HAS(c.kLights, SAIL_AREA) &&
-                       HAS(c.kShapes, SAIL_SPHERE);
-  V3 usph = v3s(0.0f);
-  if (lshared && (cat == SAIL_POINT ||
-                  (cat == SAIL_AREA &&
-                   (c.rowCopy ? c.cprims[c.lightObjRow[row]] : PRIM(c, c.lightObjRow[row])).type == SAIL_SPHERE)))
-    usph = uniformSampleSphere(u2);
   if (cat == SAIL_AREA && HAS(c.kLights, SAIL_AREA)) {  // light/area.glsl
     const V3 em = v3(L[2], L[3], L[4]);
     V3 normal; float pdf;
-    const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf, lshared ? &usph : nullptr);
+    const V3 p = sampleGeometry(c, u2, c.lightObjRow[row], normal, pdf);
     toLight = p - ins.hit;
     const V3 nt = normalize(toLight);
     contrib = em * fmax_(0.0f, dot(normal, -nt)) * fmax_(0.0f, dot(nt, ins.normal)) / pdf;
     lit = true;
   } else if (cat == SAIL_POINT && HAS(c.kLights, SAIL_POINT)) {  // light/point.glsl:13-20
     const V3 from = v3(L[1], L[2], L[3]), em = v3(L[4], L[5], L[6]);
-    const V3 p = from + (lshared ? usph : uniformSampleSphere(u2)) * 0.1f;
+    const V3 p = from + uniformSampleSphere(u2) * 0.1f;
     toLight = p - ins.hit;
     contrib = em * fmax_(0.0f, dot(normalize(toLight), ins.normal));
     lit = true;
@@ -1741,19 +1414,16 @@ D LightPrep lightPrep(const Ctx& c, const Hit& ins, V2 u2) {
   lp.lit = lit; lp.contrib = contrib; lp.toLight = toLight;
   return lp;
 }
-// SAIL_SHADOW_ZERO: a light sample whose unoccluded contribution is exactly +0 in every channel (the sample behind
+// Dead shadow tests: a light sample whose unoccluded contribution is exactly +0 in every channel (the sample behind
 // the surface or the light facing away, a spot light's falloff 0) returns that +0 vector whether or not its shadow
 // ray is blocked, so the shadow sweep is skipped; any other value (-0, NaN, a nonzero channel) takes the sweep
-#ifndef SAIL_SHADOW_ZERO
-#define SAIL_SHADOW_ZERO 1
-#endif
 D bool posZero3(const V3& v) {
   return (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
 }
 D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
   const LightPrep lp = lightPrep(c, ins, u2);
   if (!lp.lit) return v3s(0.0f);
-  if (SAIL_SHADOW_ZERO && posZero3(lp.contrib)) return v3s(0.0f);
+  if (posZero3(lp.contrib)) return v3s(0.0f);
   // testShadow(Ray(hit, toLight)) (shader.light.js:24-31): unnormalised direction, no origin offset
   if (testShadow(c, mkRay(ins.hit, lp.toLight))) return v3s(0.0f);
   return lp.contrib;
@@ -1767,11 +1437,7 @@ D V3 lightSample(const Ctx& c, const Hit& ins, V2 u2) {
 // path when a light plugin is compiled in (its light sample and shadow sweep stay in shadeBounce alone: a second
 // inlined shadow sweep multiplied the pre-cull kernel's spills).
 // Measured bit-identical: C2 +4.2 %, C3 +2.6 %, C4 -0.6 % (its 12-bounce paths are mostly matte with lights, which
-// decline). 1 (default) = every kernel but the pre-cull one, 2 = every kernel, 0 = off.
-#ifndef SAIL_LAST_BOUNCE
-#define SAIL_LAST_BOUNCE 1
-#endif
-#define SAIL_LAST_ON(cull) (SAIL_LAST_BOUNCE == 2 || (SAIL_LAST_BOUNCE == 1 && !(cull)))
+// decline), so every kernel but the pre-cull one takes it.
 D bool shadeLast(const Ctx& c, const Hit& ins, float seed, const V3& fpdf, V3& e) {
   const bool matteLit = isBlack(ins.emission) && ins.matCategory == SAIL_MATTE;  // path.glsl:10-11
   if (matteLit && c.kLights != 0) return false;
@@ -1792,33 +1458,6 @@ D bool shadeLast(const Ctx& c, const Hit& ins, float seed, const V3& fpdf, V3& e
 }
 
 // ---- path.glsl:1-38 ------------------------------------------------------------------------------------------------
-D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc);
-// fstrace.glsl:15-16 AOVs (normal/2 + 0.5, normalize(p)) of the first hit; a primary miss stores n = p = 0
-D void storeAov(float4* aovN, float4* aovP, size_t g, V3 n, V3 p) {
-  const V3 qn = n / 2.0f + 0.5f, qp = normalize(p);
-  if (aovN) aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
-  if (aovP) aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
-}
-// aovPix >= 0: this sample's first hit is stored as the pixel's AOVs (written at once, not carried in registers)
-D V3 trace(const Ctx& c, Ray ray, float tss, int maxDepth, float4* aovN, float4* aovP, long long aovPix,
-           unsigned& segs, PhaseClock& pc) {
-  V3 fpdf = v3s(1.0f), e = v3s(0.0f);
-  for (int depth = 1; depth <= maxDepth; depth++) {
-    segs++;
-    const Hit ins = intersectObjects(c, ray, depth == 1, pc);
-    PHASE_MARK(pc, 1);  // hit record of the winner
-    const float seed = tss + (float)depth;
-    if (depth == 1 && aovPix >= 0) {
-      const bool hit = ins.d < kMaxDistance;
-      storeAov(aovN, aovP, (size_t)aovPix, hit ? ins.normal : v3s(0.0f), hit ? ins.hit : v3s(0.0f));
-    }
-    if (ins.d >= kMaxDistance) break;
-    if (!(SAIL_LAST_ON(c.cullPrims) && depth == maxDepth && shadeLast(c, ins, seed, fpdf, e)))
-      shadeBounce(c, ins, ray, seed, fpdf, e, pc);
-  }
-  return e;
-}
-
 // shade() (path.glsl:1-14) + the bounce bookkeeping of trace() (path.glsl:27-36): radiance, throughput, next ray
 // A lit matte path's light sample whose shadow test is left to a later pass (the wavefront split, SAIL_DEBUG_WAVEFRONT):
 // everything the radiance update e += (emission + light * f) * fpdf needs once the shadow ray's answer is known
@@ -1836,7 +1475,6 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
     // worldToLocal(-ray.d, normal, ss, ts): its z is dot(-d, +-n) = -+(n.d) exactly (negated products, symmetric
     // rounding), already known from the hit record's into test
     const V3 nd3 = -ray.d;
-#if SAIL_AXIS_FRAME
     V3 ss, ts, wo;
     if (ins.axis) {  // box face: unit dpdu (ss = dpdu, as below), exact products
       ss = ins.dpdu;
@@ -1848,15 +1486,6 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
       ts = cross(ins.normal, ss);
       wo = v3(dot(nd3, ss), dot(nd3, ts), ins.into ? -ins.nd : ins.nd);
     }
-#else
-#if SAIL_SS_UNIT
-    const float dd = dot(ins.dpdu, ins.dpdu);
-    const V3 ss = (dd == 1.0f) ? ins.dpdu : ins.dpdu / sqrtf_(dd), ts = cross(ins.normal, ss);
-#else
-    const V3 ss = normalize(ins.dpdu), ts = cross(ins.normal, ss);
-#endif
-    const V3 wo = v3(dot(nd3, ss), dot(nd3, ts), ins.into ? -ins.nd : ins.nd);
-#endif
     // the hash is evaluated only for materials that consume it (matte/metal/glass; mirror is deterministic)
     PHASE_MARK(pc, 2);  // shading frame
     const V2 u2 = (ins.matCategory != SAIL_MIRROR) ? random2(c, seed) : v2(0.0f, 0.0f);
@@ -1864,11 +1493,7 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
     V3 wiL, f;
     const V3 mat = material(c, ins, u2, wo, wiL, f);
     const V3 _fpdf = vclamp01(mat);
-#if SAIL_AXIS_FRAME
     const V3 wi = ins.axis ? localToWorldX(wiL, ins.normal, ss, ts) : localToWorld(wiL, ins.normal, ss, ts);
-#else
-    const V3 wi = localToWorld(wiL, ins.normal, ss, ts);
-#endif
     PHASE_MARK(pc, 4);  // BSDF sample
     V3 direct = v3s(0.0f);
     bool deferE = false;
@@ -1878,7 +1503,7 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
         direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
       } else if (DEFER) {  // lightSample's light prep now, its shadow test and the radiance update in the shadow pass
         const LightPrep lp = lightPrep(c, ins, u2);
-        if (lp.lit && !(SAIL_SHADOW_ZERO && posZero3(lp.contrib))) {
+        if (lp.lit && !posZero3(lp.contrib)) {
           sp->pending = true; sp->contrib = lp.contrib; sp->toLight = lp.toLight; sp->hit = ins.hit; sp->f = f;
           sp->emission = ins.emission; sp->fpdfOld = fpdf;
           deferE = true;
@@ -1895,11 +1520,7 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
       e = e + sh * fpdf;
     }
     fpdf = fpdf * _fpdf;
-#if SAIL_AXIS_FRAME
     const float outdot = ins.axis ? dotX(ins.normal, wi) : dot(ins.normal, wi);
-#else
-    const float outdot = dot(ins.normal, wi);
-#endif
     ray = mkRay(ins.hit + ins.normal * (outdot > kEps ? 0.0001f : -0.0001f), wi);
     PHASE_MARK(pc, 6);  // next ray
   }
@@ -1968,195 +1589,49 @@ D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
 
 }  // namespace
 
-// 256 threads = 16x16 pixel block; wave w covers the 16x4 strip rows 4w..4w+3; 16 blocks per 64x64 tile.
-#ifndef SAIL_TRACE_MIN_WAVES
-#define SAIL_TRACE_MIN_WAVES 6
-#endif
-// CULL selects the padded-box pre-cull at compile time (two kernels), so small scenes carry none of its code.
-template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL>
-__device__ __forceinline__ void traceTile(const SailTraceArgs& A) {
-  const TileWork tw = tileWork<GROUPED>(A);
-  const int ownedTile = tw.ownedTile;
-  const int sub = tw.sub;
-  const int tile = A.rank + ownedTile * A.world;
-  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int x = tx * 64 + (sub & 3) * 16 + (lane & 15);
-  const int y = ty * 64 + (sub >> 2) * 16 + wave * 4 + (lane >> 4);
-#if SAIL_PRIMS_LDS
-  // stage the decoded primitives in LDS once per workgroup; reads are then wave-uniform ds_reads
-  __shared__ SailPrim sPrims[SAIL_PRIMS_LDS];
-  {
-    const float4* src = reinterpret_cast<const float4*>(A.prims);
-    float4* dst = reinterpret_cast<float4*>(sPrims);
-    const int nv = A.n * (int)(sizeof(SailPrim) / sizeof(float4));
-    for (int i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
-    __syncthreads();
-  }
-#endif
-  if (x >= A.W || y >= A.H || ownedTile >= A.ownedTiles) return;
-
-  Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
-#if SAIL_PRIMS_LDS
-  c.prims = sPrims;
-#else
-  c.prims = A.prims;
-  c.cprims = A.prims;
-  c.tpl = A.texparams;
-  c.rowCopy = false;
-  c.tpCopy = false;
-#endif
-  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
-  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
-  c.fcx = (float)x + 0.5f; c.fcy = (float)y + 0.5f;
-  c.shadowAnyHit = A.shadowAnyHit;
-  c.cullPrims = CULL ? 1 : 0;
-  c.cullFma = CULL && A.cullPrims == 2;
-  c.cullPrimary = A.cullPrimary;
-  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
-
-  const size_t pix = (size_t)y * A.W + x;
-  constexpr bool grouped = GROUPED;
-  // per-pixel state that is only touched once per sample lives in LDS, not in registers across the bounces
-  // (the pre-cull kernel is register-bound: every freed VGPR is spill traffic saved)
-  __shared__ float4 sAcc[256];
-  __shared__ float2 sST[256];
-  const int li = threadIdx.x;
-  const bool home = !grouped;  // the generic kernel's groups all stage (SAIL_GROUP_HOME_FOR)
-  sAcc[li] = home ? A.accum[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  sST[li] = make_float2(((float)x + 0.5f) / (float)A.W, ((float)y + 0.5f) / (float)A.H);
-  const bool aovGroup = tw.kEnd == A.spp;  // the group holding the launch's last sample writes the AOVs
-  const bool wantAov = (A.aovN || A.aovP) && aovGroup;
-  unsigned segs = 0;
-  PhaseClock pc;
-#if SAIL_PHASE_TIMING
-  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
-  pc.t = __builtin_amdgcn_s_memtime();
-#endif
-  for (int k = tw.kBeg; k < tw.kEnd; k++) {
-    const SailSample& S = constRow<SailSample>(A.samples, k);
-    const float s = sST[li].x, t = sST[li].y;
-    const bool tri0 = s + t <= 1.0f;
-    const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
-    const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
-    const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
-    const Ray ray = mkRay(eye, tri0 ? (d0 + (d2 - d0) * s + (d1 - d0) * t) : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
-    const long long aovPix = (wantAov && k == A.spp - 1) ? (long long)pix : -1;
-    const V3 e = trace(c, ray, S.seed, A.maxBounces, A.aovN, A.aovP, aovPix, segs, pc);
-    if (!home) stageSample(A, k, tw.bid, threadIdx.x, e);
-    else { float4 acc = sAcc[li]; accumulateSample(acc, e, S, A.accumMode); sAcc[li] = acc; }
-  }
-  if (home) A.accum[pix] = sAcc[li];
-#if SAIL_PHASE_TIMING
-  PHASE_MARK(pc, 7);  // accumulate + store
-  if (lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
-#endif
-  if (A.segCounter) {
-    // one atomic per wave: sum the lanes' segment counts with a cross-lane reduction; the waves spread their
-    // atomics over kSegSlots counters (one address took ~0.2 ms per 1080p launch in contended atomics)
-    unsigned long long v = segs;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
-  }
-}
 // Path compaction: after every primitive sweep the workgroup's 256 live paths are sorted through LDS by
 // (shape type, material) so that the hit record and the shading, the divergent half of a bounce, run on
 // waves of like paths; dead paths drop out, so whole waves idle past the end of the live range. A path's
 // state (ray, throughput, radiance, pixel, sweep result: 18 words) migrates between lanes; every path's
 // arithmetic is unchanged, so the result is bit-identical to the unsorted kernel. The radiance of a sample
 // goes back to the pixel's own lane through LDS before it is accumulated, in sample order.
-#ifndef SAIL_COMPACT
-#define SAIL_COMPACT 1
-#endif
-#ifndef SAIL_SORT_BY_PRIM
-#define SAIL_SORT_BY_PRIM 1
-#endif
-// the (shape, material) key material-major: matte paths, which alone run the light sample and its shadow sweep,
-// share waves (C4 +5.2 %; ordering the by-row key the same way through a host rank table: C3 -2.8 %, not adopted)
-#ifndef SAIL_SORT_MATMAJOR
-#define SAIL_SORT_MATMAJOR 1
-#endif
-// SAIL_PRIO_MIXED = p: after the sort, a wave whose live paths have different sort keys runs at issue priority p
-// (variants in gpurun_out/r03f: C3 +7.3 % alone)
-#ifndef SAIL_PRIO_MIXED
-#define SAIL_PRIO_MIXED 2
-#endif
-#ifndef SAIL_PRIO_MATTE
-#define SAIL_PRIO_MATTE 0
-#endif
-// SAIL_STATE_PACK (SAIL_STATE_PACK_CULL for the pre-cull kernel): the migrated path state as 15 floats (0), six float2
-// (1, ds_*_b64) or three float4 (2, ds_*_b128), the local hit point recomputed when packed; SAIL_E4 (_CULL): each
-// pixel's radiance slot as one float4. Measured with priority 2 (gpurun_out/r03g, Gseg/s C1 / C3 / C4): pack 1
-// 89.6 / 29.0 / 9.40, pack 2 90.0 / 29.0 / 9.10, pack 1 + E4 90.1 / 29.15 / 9.10, pack 2 + E4 90.3 / 29.15 / 9.10
-// (no packing, no priority: 86.0 / 26.3 / 9.04)
-#ifndef SAIL_STATE_PACK
-#define SAIL_STATE_PACK 2
-#endif
-#ifndef SAIL_E4
-#define SAIL_E4 1
-#endif
-#ifndef SAIL_STATE_PACK_CULL
-#define SAIL_STATE_PACK_CULL 1
-#endif
-#ifndef SAIL_E4_CULL
-#define SAIL_E4_CULL 0
-#endif
-// the sort's prefix sum over the key counts: 1 = by DPP (sail_scan.h, six VALU, no LDS round trips), 0 = shuffles
-#ifndef SAIL_SCAN_DPP
-#define SAIL_SCAN_DPP 1
-#endif
-// SAIL_END_DEFER: no end-of-sample barriers. Sample k's radiance is read back by its pixel's lane after the first
-// sort barrier of sample k + 1 (every write of sample k precedes it; sample k + 1 writes the slot only after the
-// scatter barrier), the first bounce starts from 0 instead of a cleared slot, and a path that misses at once clears
-// its own slot there. The last sample is read after one barrier at the end. Bit-identical, measured slower (the
-// read-back and accumulation inlined into the bounce loop: C2 -2.3 %, C3 -6.6 %, C4 -2.2 %), so off.
-#ifndef SAIL_END_DEFER
-#define SAIL_END_DEFER 0
-#endif
-// SAIL_SORT_2BAR: two barriers per bounce instead of three (every wave scans double-buffered counts itself):
-// 1 = every kernel, 2 = the pre-cull kernel only, 3 = the pre-cull and room kernels. Bit-identical; measured with the
-// shuffle scan C2 -3.4 %, C3 -0.5 %, C4 +0.9 %; with the DPP scan and the live count by readlane C2 -1.0 %, C3 +1.1 %
-// (twice), C4 +1.3-1.7 % over the bpermute count
-#ifndef SAIL_SORT_2BAR
-#define SAIL_SORT_2BAR 3
-#endif
-// SAIL_CULL_LDS_ROWS: scenes of at most this many rows are copied into LDS by each pre-cull workgroup, and the
-// candidate loops read their per-lane rows from there instead of global memory (0 = off). C4 +4.3 %; with the hit
-// record's and light sampler's rows and the texParams table there too (SAIL_CULL_LDS_HIT / _TP) +8.8 %
-// (gpurun_out/r03aa, r03ab). 72 rows + 136 texParams rows keep the block at 79.9 KB: two 1,024-thread workgroups
-// per CU.
-#ifndef SAIL_CULL_LDS_ROWS
-#define SAIL_CULL_LDS_ROWS 72
-#endif
-// SAIL_SHADOW_COMPACT: lit matte paths leave their shadow rays in the sort buffer (compacted, after a barrier that
-// ends the bounce's gathers) and the workgroup's first threads trace them, so waves whose lanes have no shadow ray
-// (non-matte, unlit, contribution +0) do no shadow sweep; the radiance slot holds the shadowed outcome until the
-// tracing thread writes the lit one. 1 = the pre-cull kernel, 2 = the pre-cull and room kernels, 0 = off. Measured
-// (gpurun_out/r03m, bit-identical): C4 +3.1 % (spills 74 -> 105 VGPRs), C3 -25 % (room spills 41 -> 85).
-#ifndef SAIL_SHADOW_COMPACT
-#define SAIL_SHADOW_COMPACT 1
-#endif
-#ifndef SAIL_PROBE_MAJORITY
-#define SAIL_PROBE_MAJORITY 0
-#endif
-// NT threads per workgroup (ungrouped kernels only; grouped ones keep 256): a 16 x NT/16 pixel block, 4096/NT
-// blocks per 64x64 tile. A larger workgroup sorts a larger pool of paths (fewer mixed waves) at the price of a
-// wider barrier.
+// The sort key is the winning primitive row for scenes of fewer than 64 rows, else (material, shape) material-major:
+// matte paths, which alone run the light sample and its shadow sweep, share waves (C4 +5.2 %; ordering the by-row key
+// the same way through a host rank table: C3 -2.8 %).
+// After the sort, a wave whose live paths have different sort keys runs at issue priority kPrioMixed (C3 +7.3 %).
+// Path state moves through LDS packed: three float4 per path in the flat kernels (ds_*_b128), six float2 in the
+// pre-cull kernel (ds_*_b64), the local hit point recomputed; the flat kernels keep each pixel's radiance as one float4
+// (measured with priority 2, Gseg/s C1 / C3 / C4: six float2 89.6 / 29.0 / 9.40, three float4 90.0 / 29.0 / 9.10,
+// + float4 radiance 90.1 / 29.15 / 9.10 and 90.3 / 29.15 / 9.10; unpacked, no priority 86.0 / 26.3 / 9.04).
+// The sort's prefix sum over the key counts is six DPP adds (sail_scan.h).
+// Barriers per bounce: two in the pre-cull and room kernels (every wave scans double-buffered counts itself), three in
+// the Cornell kernel (one wave scans). Bit-identical; with the DPP scan and the live count by readlane C2 -1.0 % with
+// two, C3 +1.1 % (twice), C4 +1.3-1.7 %. Deferring each sample's read-back past the next sample's first barrier (no
+// end-of-sample barriers) was bit-identical and slower: C2 -2.3 %, C3 -6.6 %, C4 -2.2 %.
+// The pre-cull kernel copies scenes of at most kCullLdsRows rows into LDS per workgroup, and its candidate loops, hit
+// record and light sampler read their per-lane rows from there (C4 +4.3 %), with texParams tables of at most
+// kCullLdsTp rows as well (+8.8 % together). 72 + 136 rows keep the block at 79.9 KB: two 1,024-thread workgroups per
+// CU. The same copies in the flat kernels lost (C2 -6 %, C3 +-0).
+// Compacted shadow rays (pre-cull kernel): lit matte paths leave their shadow rays in the sort buffer (compacted, after
+// a barrier that ends the bounce's gathers) and the workgroup's first threads trace them, so waves whose lanes have no
+// shadow ray (non-matte, unlit, contribution +0) do no shadow sweep; the radiance slot holds the shadowed outcome until
+// the tracing thread writes the lit one. Measured (gpurun_out/r03m, bit-identical): C4 +3.1 % (spills 74 -> 105
+// VGPRs); in the room kernel C3 -25 % (its spills 41 -> 85).
+// NT threads per workgroup: a 16 x NT/16 pixel block, 4096/NT blocks per 64x64 tile. A larger workgroup sorts a
+// larger pool of paths (fewer mixed waves) at the price of a wider barrier.
+constexpr int kCullLdsRows = 72, kCullLdsTp = 136;
+constexpr int kPrioMixed = 2;
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
-  constexpr int kFields = 15;
-  constexpr int kPack = CULL ? SAIL_STATE_PACK_CULL : SAIL_STATE_PACK;
-  constexpr bool kE4 = CULL ? SAIL_E4_CULL : SAIL_E4;
+  constexpr int kPack = CULL ? 1 : 2;
+  constexpr bool kE4 = !CULL;
   // packed path state, 2: three float4 per path -- ray o + d.x, d.yz + throughput.xy, throughput.z + distance +
   // pixel | row << 10 + key (ds_write_b128 / ds_read_b128: 3 + 3 LDS instructions instead of 15 + 15); 1: six
-  // float2 (ds_*_b64); the local hit point is recomputed (hitRecord<true>). Unused forms are one element.
+  // float2 (ds_*_b64); the local hit point is recomputed (hitRecord<true>). The unused form is one element.
   __shared__ float4 sSt4[kPack == 2 ? 3 : 1][kPack == 2 ? NT : 1];
   __shared__ float2 sSt2[kPack == 1 ? 6 : 1][kPack == 1 ? NT : 1];
-  __shared__ float sSt[kPack == 0 ? kFields : 1][kPack == 0 ? NT : 1];
   // each pixel's radiance: one float4 (one ds_read_b128 / ds_write_b128) or three floats
   __shared__ float4 sE4[kE4 ? NT : 1];
   __shared__ float sE[kE4 ? 1 : 3][kE4 ? 1 : NT];
@@ -2168,12 +1643,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if constexpr (kE4) sE4[i] = make_float4(v.x, v.y, v.z, 0.0f);
     else { sE[0][i] = v.x; sE[1][i] = v.y; sE[2][i] = v.z; }
   };
-  constexpr bool kShCompact = SAIL_SHADOW_COMPACT >= 1 && KL != 0u &&
-                              (CULL || (SAIL_SHADOW_COMPACT >= 2 && KS == SAIL_KSET_ROOM_SHAPES));
+  constexpr bool kShCompact = CULL && KL != 0u;
   __shared__ int sShCnt[2];
   int shph = 0;
-  constexpr bool twoBar = SAIL_SORT_2BAR == 1 || (SAIL_SORT_2BAR >= 2 && CULL) ||
-                          (SAIL_SORT_2BAR == 3 && KS == SAIL_KSET_ROOM_SHAPES && !CULL);
+  constexpr bool twoBar = CULL || KS == SAIL_KSET_ROOM_SHAPES;
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
   const TileWork tw = tileWork<GROUPED, NT>(A);
@@ -2203,17 +1676,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.cullPrimary = A.cullPrimary;
   c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
 
-#if SAIL_CULL_AGPR
-  // AGPRs in use: the allocator splits the 64-register budget into 32 VGPRs + 32 AGPRs and spills to the AGPRs
-  // (1,128 v_accvgpr moves, 103 scratch instructions instead of 94): bit-identical, C4 -8 %. Off.
-  if (CULL) __asm__ volatile("" ::: "a0");
-#endif
   if (li < (twoBar ? 2 : 1) * kKeys) sCnt2[li / kKeys][li % kKeys] = 0;
   if (li < 2) sShCnt[li] = 0;
-  // the pre-cull kernel's candidate loops read rows per lane: from an LDS copy of the scene when it fits (and the
-  // flat kernels' per-lane hit-record, light-sampler and texParams reads with SAIL_FLAT_LDS)
-  constexpr int kLdsRows = CULL ? SAIL_CULL_LDS_ROWS : SAIL_FLAT_LDS;
-  c.rowCopy = CULL ? (SAIL_CULL_LDS_HIT != 0) : (SAIL_FLAT_LDS != 0);
+  // the pre-cull kernel's candidate loops, hit record and light sampler read rows per lane: from an LDS copy of the
+  // scene when it fits
+  constexpr int kLdsRows = CULL ? kCullLdsRows : 0;
+  c.rowCopy = CULL;
   __shared__ float4 sPrimL[kLdsRows > 0 ? kLdsRows * (int)(sizeof(SailPrim) / 16) : 1];
   if constexpr (kLdsRows > 0) {
     if (A.n <= kLdsRows) {  // uniform
@@ -2223,15 +1691,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       c.cprims = reinterpret_cast<const SailPrim*>(sPrimL);
     }
   }
-  constexpr int kLdsLights = CULL ? SAIL_CULL_LDS_LIGHTS : 0;  // light rows (18 floats) read per lane
-  __shared__ float sLtL[kLdsLights > 0 ? kLdsLights * 18 : 1];
-  if constexpr (kLdsLights > 0) {
-    if (A.ln <= kLdsLights) {  // uniform
-      for (int i = li; i < A.ln * 18; i += NT) sLtL[i] = A.lights[i];
-      c.lt = sLtL;
-    }
-  }
-  constexpr int kLdsTp = CULL ? SAIL_CULL_LDS_TP : (SAIL_FLAT_LDS ? SAIL_FLAT_LDS_TP : 0);
+  constexpr int kLdsTp = CULL ? kCullLdsTp : 0;
   c.tpCopy = kLdsTp > 0;
   __shared__ float4 sTpL[kLdsTp > 0 ? kLdsTp * 4 : 1];
   if constexpr (kLdsTp > 0) {
@@ -2247,11 +1707,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   // paths share their primitive and material rows; C2 +3.7 %, C3 +1.2 %), else (shape type, material category).
   // A waterfall over the wave's rows with the row index in an SGPR (scalar row loads) was measured: the
   // duplicated shading body doubled the spills, C2 -40 %.
-  const bool byPrim = SAIL_SORT_BY_PRIM && A.n < kKeys;
+  const bool byPrim = A.n < kKeys;
   const size_t pixG = (size_t)y * A.W + x;
   constexpr bool grouped = GROUPED;
   // the room kernel's first group accumulates its samples itself (SAIL_GROUP_HOME_FOR, sail_device.h)
-  constexpr bool kHome = SAIL_GROUP_HOME && KS == SAIL_KSET_ROOM_SHAPES && !CULL;
+  constexpr bool kHome = KS == SAIL_KSET_ROOM_SHAPES && !CULL;
   const bool home = !grouped || (kHome && tw.kBeg == 0);
   float4 acc = (valid && home) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
@@ -2263,18 +1723,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   for (int q = 0; q < 8; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
-  // SAIL_END_DEFER (needs a first bounce, whose sort barrier orders the read-back)
-  const bool deferRead = SAIL_END_DEFER && A.maxBounces >= 1;
-  int kPrev = -1;
-  // sample kPrev's radiance into the accumulator / stage; a path that missed at once (dead) clears its slot
-  auto settlePrev = [&](bool alive) {
-    if (valid && kPrev >= 0) {
-      const V3 er = E_LOAD(li);
-      if (!home) stageSample<NT>(A, kPrev, tw.bid, li, er);
-      else accumulateSample(acc, er, constRow<SailSample>(A.samples, kPrev), A.accumMode);
-    }
-    if (!alive) E_STORE(li, v3s(0.0f));
-  };
   for (int k = tw.kBeg; k < tw.kEnd; k++) {
     const SailSample& S = constRow<SailSample>(A.samples, k);
     const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
@@ -2288,7 +1736,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     }
     V3 fpdf = v3s(1.0f);
     // the path's radiance lives in LDS at its pixel: one path per pixel, updated in bounce order
-    if (!deferRead) E_STORE(li, v3s(0.0f));
+    E_STORE(li, v3s(0.0f));
     for (int depth = 1; depth <= A.maxBounces; depth++) {
       Sweep sw;
       sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
@@ -2310,11 +1758,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           const SailPrim& p = PRIM(c, sw.bi);
           int mc = matCat(p);
           mc = (mc >= 0 && mc < 5) ? mc : 0;
-#if SAIL_SORT_MATMAJOR
           key = 1 + mc * 10 + p.type;
-#else
-          key = 1 + p.type * 5 + mc;
-#endif
         }
       }
       PHASE_MARK(pc, 0);
@@ -2327,17 +1771,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           sSt4[0][d] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
           sSt4[1][d] = make_float4(ray.d.y, ray.d.z, fpdf.x, fpdf.y);
           sSt4[2][d] = make_float4(fpdf.z, sw.best, __int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
-        } else if constexpr (kPack == 1) {
+        } else {
           sSt2[0][d] = make_float2(ray.o.x, ray.o.y); sSt2[1][d] = make_float2(ray.o.z, ray.d.x);
           sSt2[2][d] = make_float2(ray.d.y, ray.d.z); sSt2[3][d] = make_float2(fpdf.x, fpdf.y);
           sSt2[4][d] = make_float2(fpdf.z, sw.best);
           sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
-        } else {
-          sSt[0][d] = ray.o.x; sSt[1][d] = ray.o.y; sSt[2][d] = ray.o.z;
-          sSt[3][d] = ray.d.x; sSt[4][d] = ray.d.y; sSt[5][d] = ray.d.z;
-          sSt[6][d] = fpdf.x; sSt[7][d] = fpdf.y; sSt[8][d] = fpdf.z;
-          sSt[9][d] = __int_as_float(pixel); sSt[10][d] = __int_as_float(sw.bi); sSt[11][d] = sw.best;
-          sSt[12][d] = sw.bhl.x; sSt[13][d] = sw.bhl.y; sSt[14][d] = sw.bhl.z;
         }
       };
       if constexpr (twoBar) {
@@ -2346,18 +1784,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       // cleared by wave 0 after the scatter barrier, two bounces before it is counted into again
       if (alive) rank = atomicAdd(&sCnt2[ph][key], 1);
       __syncthreads();
-      if (deferRead && depth == 1) settlePrev(alive);
       {
         const int v = sCnt2[ph][lane];
-#if SAIL_SCAN_DPP
         const int incl = waveScanIncl(v);
-#else
-        int incl = v;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int u = __shfl_up(incl, off, 64);
-          if (lane >= off) incl += u;
-        }
-#endif
         nAlive = __builtin_amdgcn_readlane(incl, 63);
         const int start = __shfl(incl - v, key, 64);
         if (alive) scatterTo(start + rank);
@@ -2369,18 +1798,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int* const sCnt = sCnt2[0];
       if (alive) rank = atomicAdd(&sCnt[key], 1);
       __syncthreads();
-      if (deferRead && depth == 1) settlePrev(alive);
       if (wave == 0) {
         const int v = sCnt[lane];
-#if SAIL_SCAN_DPP
         const int incl = waveScanIncl(v);
-#else
-        int incl = v;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int u = __shfl_up(incl, off, 64);
-          if (lane >= off) incl += u;
-        }
-#endif
         sStart[lane] = incl - v;
         if (lane == 63) sStart[kKeys] = incl;
         sCnt[lane] = 0;
@@ -2394,8 +1814,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       ShadowPending sp;
       sp.pending = false;
       V3 eLit = v3s(0.0f);
-      int keyG = 0;  // the gathered path's sort key (packed state only)
-      (void)keyG;
+      int keyG = 0;  // the gathered path's sort key
       PHASE_MARK(pc, 7);
       if (alive) {
         if constexpr (kPack == 2) {
@@ -2409,7 +1828,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           pixel = pk & 1023;
           sw.bi = pk >> 10;
           sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
-        } else if constexpr (kPack == 1) {
+        } else {
           const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
           const int pk = __float_as_int(sSt2[5][li].x);
           keyG = __float_as_int(sSt2[5][li].y);
@@ -2420,43 +1839,18 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           pixel = pk & 1023;
           sw.bi = pk >> 10;
           sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
-        } else {
-          ray.o = v3(sSt[0][li], sSt[1][li], sSt[2][li]);
-          ray.d = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
-          fpdf = v3(sSt[6][li], sSt[7][li], sSt[8][li]);
-          pixel = __float_as_int(sSt[9][li]);
-          sw.bi = __float_as_int(sSt[10][li]); sw.best = sSt[11][li];
-          sw.bhl = v3(sSt[12][li], sSt[13][li], sSt[14][li]);
         }
         ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
-        bool mixedW = false;
-        (void)mixedW;
-#if SAIL_PRIO_MIXED
         {  // a wave whose live paths have different sort keys runs several hit-record / material branches: raise its
            // issue priority so that its workgroup's next barrier is not held up by it (the other waves wait there)
-          const int kk = kPack ? keyG : sw.bi;
-          const int k0 = __builtin_amdgcn_readfirstlane(kk);
-          mixedW = __builtin_amdgcn_ballot_w64(kk != k0) != 0ull;
-          if (mixedW) __builtin_amdgcn_s_setprio(SAIL_PRIO_MIXED);
+          const int k0 = __builtin_amdgcn_readfirstlane(keyG);
+          const bool mixedW = __builtin_amdgcn_ballot_w64(keyG != k0) != 0ull;
+          if (mixedW) __builtin_amdgcn_s_setprio(kPrioMixed);
           else __builtin_amdgcn_s_setprio(0);
         }
-#endif
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
-#if SAIL_PROBE_MAJORITY
-        // timing probe only (not bit-exact): lanes whose key differs from lane 32's skip this bounce's shading
-        const int kMid = __builtin_amdgcn_readlane(kPack ? keyG : sw.bi, 32);
-        const unsigned long long midM = __builtin_amdgcn_ballot_w64((kPack ? keyG : sw.bi) == kMid);
-        if ((kPack ? keyG : sw.bi) == kMid || midM == 0ull) {
-#endif
-        const Hit ins = hitRecordU<kPack != 0>(c, ray, sw);
-#if SAIL_PRIO_MATTE
-        // study: a uniform wave of lit matte paths (light sample + shadow sweep ahead, the longest bounce) at
-        // priority SAIL_PRIO_MATTE
-        if (KL != 0u && !mixedW &&
-            __builtin_amdgcn_ballot_w64(isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) != 0ull)
-          __builtin_amdgcn_s_setprio(SAIL_PRIO_MATTE);
-#endif
+        const Hit ins = hitRecordU<true>(c, ray, sw);
         PHASE_MARK(pc, 1);
         if (depth == 1 && aovSample) {
           const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
@@ -2464,8 +1858,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
-        V3 e = (deferRead && depth == 1) ? v3s(0.0f) : E_LOAD(pixel);
-        if (!(SAIL_LAST_ON(CULL) && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e))) {
+        V3 e = E_LOAD(pixel);
+        if (!(!CULL && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e))) {
           if constexpr (kShCompact) {
             shadeBounceT<true>(c, ins, ray, S.seed + (float)depth, fpdf, e, pc, &sp);
             if (sp.pending) {  // both outcomes of e += (emission + (0 + light * f)) * throughput, as shadeBounce
@@ -2480,9 +1874,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           }
         }
         E_STORE(pixel, e);
-#if SAIL_PROBE_MAJORITY
-        }
-#endif
       }
       if constexpr (kShCompact) {
         if (c.ln > 0) {  // uniform
@@ -2501,14 +1892,10 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
                 sSt4[0][d] = make_float4(o.x, o.y, o.z, dl.x);
                 sSt4[1][d] = make_float4(dl.y, dl.z, eLit.x, eLit.y);
                 sSt4[2][d] = make_float4(eLit.z, __int_as_float(pixel), 0.0f, 0.0f);
-              } else if constexpr (kPack == 1) {
+              } else {
                 sSt2[0][d] = make_float2(o.x, o.y); sSt2[1][d] = make_float2(o.z, dl.x);
                 sSt2[2][d] = make_float2(dl.y, dl.z); sSt2[3][d] = make_float2(eLit.x, eLit.y);
                 sSt2[4][d] = make_float2(eLit.z, __int_as_float(pixel));
-              } else {
-                sSt[0][d] = o.x; sSt[1][d] = o.y; sSt[2][d] = o.z; sSt[3][d] = dl.x; sSt[4][d] = dl.y;
-                sSt[5][d] = dl.z; sSt[6][d] = eLit.x; sSt[7][d] = eLit.y; sSt[8][d] = eLit.z;
-                sSt[9][d] = __int_as_float(pixel);
               }
             }
           }
@@ -2523,20 +1910,16 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
               const float4 q0 = sSt4[0][li], q1 = sSt4[1][li], q2 = sSt4[2][li];
               o = v3(q0.x, q0.y, q0.z); dl = v3(q0.w, q1.x, q1.y); el = v3(q1.z, q1.w, q2.x);
               pix = __float_as_int(q2.y);
-            } else if constexpr (kPack == 1) {
+            } else {
               const float2 q0 = sSt2[0][li], q1 = sSt2[1][li], q2 = sSt2[2][li], q3 = sSt2[3][li], q4 = sSt2[4][li];
               o = v3(q0.x, q0.y, q1.x); dl = v3(q1.y, q2.x, q2.y); el = v3(q3.x, q3.y, q4.x);
               pix = __float_as_int(q4.y);
-            } else {
-              o = v3(sSt[0][li], sSt[1][li], sSt[2][li]); dl = v3(sSt[3][li], sSt[4][li], sSt[5][li]);
-              el = v3(sSt[6][li], sSt[7][li], sSt[8][li]); pix = __float_as_int(sSt[9][li]);
             }
             if (!testShadow(c, mkRay(o, dl))) E_STORE(pix, el);
           }
         }
       }
     }
-    if (deferRead) { kPrev = k; continue; }
     __syncthreads();
     if (valid) {
       const V3 er = E_LOAD(li);
@@ -2544,10 +1927,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       else accumulateSample(acc, er, S, A.accumMode);
     }
     __syncthreads();
-  }
-  if (deferRead && kPrev >= 0) {
-    __syncthreads();
-    settlePrev(true);
   }
   if (valid && home) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
@@ -2561,88 +1940,37 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   }
 }
 // Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;
-// earlier builds with more live state lost to spills in the flat kernels). SAIL_COMPACT=0 / SAIL_*_TILE select
-// the unsorted body for comparisons.
-#if SAIL_COMPACT
-#define SAIL_TILE_SMALL traceTileCompact
-#else
-#define SAIL_TILE_SMALL traceTile
-#endif
-
-// each plugin set has an ungrouped kernel (one workgroup per 16x16 block, every sample) and a _grouped one
-// (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel)
-#define SAIL_TRACE_KERNELS_NT(name, waves, body, cull, ks, km, kt, kl, nt, gnt)                                  \
+// earlier builds with more live state lost to spills in the flat kernels).
+// Each plugin set has an ungrouped kernel (one workgroup per 16 x NT/16 block, every sample) and a _grouped one
+// (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel). Launch bounds: waves per SIMD
+// and threads per workgroup, chosen by the occupancy sweeps of DESIGN.md §5 (sail_launch_trace sizes the grids).
+#define SAIL_TRACE_KERNELS(name, waves, cull, ks, km, kt, kl, nt, gnt)                                               \
   extern "C" __global__ void __launch_bounds__(nt, waves) name(SailTraceArgs A) {                                \
-    body<cull, false, ks, km, kt, kl, nt>(A);                                                                    \
+    traceTileCompact<cull, false, ks, km, kt, kl, nt>(A);                                                        \
   }                                                                                                              \
   extern "C" __global__ void __launch_bounds__(gnt, waves) name##_grouped(SailTraceArgs A) {                     \
-    body<cull, true, ks, km, kt, kl, gnt>(A);                                                                    \
+    traceTileCompact<cull, true, ks, km, kt, kl, gnt>(A);                                                        \
   }
-#define SAIL_TRACE_KERNELS(name, waves, body, cull, ks, km, kt, kl)                                              \
-  extern "C" __global__ void __launch_bounds__(256, waves) name(SailTraceArgs A) {                               \
-    body<cull, false, ks, km, kt, kl>(A);                                                                        \
-  }                                                                                                              \
-  extern "C" __global__ void __launch_bounds__(256, waves) name##_grouped(SailTraceArgs A) {                     \
-    body<cull, true, ks, km, kt, kl>(A);                                                                         \
-  }
-
-#ifndef SAIL_GENERIC_TILE
-#define SAIL_GENERIC_TILE SAIL_TILE_SMALL
-#endif
-SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_TRACE_MIN_WAVES, SAIL_GENERIC_TILE, false, ~0u, ~0u, ~0u, ~0u)
+// every plugin (any scene of fewer than 8 primitives outside the two sets below)
+#define SAIL_GENERIC_WAVES 6
+SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_GENERIC_WAVES, false, ~0u, ~0u, ~0u, ~0u, 256, 256)
 // the README Cornell box plugin set (C1/C2/C5): Cube + Sphere + Cornellbox, Matte + Mirror, uniform colours
-#ifndef SAIL_TRACE_CORNELL_MIN_WAVES
-#define SAIL_TRACE_CORNELL_MIN_WAVES 8
-#endif
-#ifndef SAIL_CORNELL_CULL
-#define SAIL_CORNELL_CULL false
-#endif
-#ifndef SAIL_CORNELL_NT
+#define SAIL_CORNELL_WAVES 8
 #define SAIL_CORNELL_NT 256
-#endif
-// threads per workgroup of the grouped flat kernels (the sort pool of a sample group's workgroup)
-#ifndef SAIL_CORNELL_GROUP_NT
 #define SAIL_CORNELL_GROUP_NT 256
-#endif
-SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cornell, SAIL_TRACE_CORNELL_MIN_WAVES, SAIL_TILE_SMALL, SAIL_CORNELL_CULL,
-                      SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS,
-                      SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT)
+SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_CORNELL_WAVES, false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS,
+                   SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT)
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
-#ifndef SAIL_TRACE_ROOM_MIN_WAVES
-#define SAIL_TRACE_ROOM_MIN_WAVES 7
-#endif
-#ifndef SAIL_ROOM_TILE
-#define SAIL_ROOM_TILE SAIL_TILE_SMALL
-#endif
-#ifndef SAIL_ROOM_CULL
-#define SAIL_ROOM_CULL false
-#endif
-#ifndef SAIL_ROOM_NT
+#define SAIL_ROOM_WAVES 7
 #define SAIL_ROOM_NT 256
-#endif
-#ifndef SAIL_ROOM_GROUP_NT
 #define SAIL_ROOM_GROUP_NT 256
-#endif
-SAIL_TRACE_KERNELS_NT(sail_trace_kernel_room, SAIL_TRACE_ROOM_MIN_WAVES, SAIL_ROOM_TILE, SAIL_ROOM_CULL,
-                      SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT,
-                      SAIL_ROOM_GROUP_NT)
-// the pre-cull kernel serves scenes with many primitives (C4: 7 waves measured best of 5-8)
-#ifndef SAIL_TRACE_CULL_MIN_WAVES
-#define SAIL_TRACE_CULL_MIN_WAVES 8
-#endif
-#ifndef SAIL_CULL_TILE
-#define SAIL_CULL_TILE SAIL_TILE_SMALL
-#endif
-// threads per workgroup of the ungrouped pre-cull kernel (sail_launch_trace sizes its grid to match)
-#ifndef SAIL_CULL_NT
+SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_ROOM_WAVES, false, SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS,
+                   SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT)
+// the pre-cull kernel serves scenes with many primitives (C4); 1,024-thread workgroups (16 x 64 strips)
+#define SAIL_CULL_WAVES 8
 #define SAIL_CULL_NT 1024
-#endif
-// threads per workgroup of the grouped pre-cull kernel (sample groups of small per-rank frames)
-#ifndef SAIL_CULL_GROUP_NT
 #define SAIL_CULL_GROUP_NT 1024
-#endif
-SAIL_TRACE_KERNELS_NT(sail_trace_kernel_cull, SAIL_TRACE_CULL_MIN_WAVES, SAIL_CULL_TILE, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT,
-                      SAIL_CULL_GROUP_NT)
+SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_CULL_WAVES, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT, SAIL_CULL_GROUP_NT)
 
 // ---- wavefront split of the pre-cull path (study switch SAIL_DEBUG_WAVEFRONT; DESIGN.md §9 of round 2) -------------------
 // The megakernel keeps each path in registers and LDS across its bounces and sorts the workgroup's paths between the
@@ -3058,7 +2386,7 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
   out[i] = r;
 }
 
-#if SAIL_PHASE_TIMING || SAIL_CULL_STATS
+#if SAIL_PHASE_TIMING
 // phase-timing readout for the variant harness (tools/variant_bench.py --phases)
 extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;

@@ -149,12 +149,15 @@ class Renderer {
     const ck = this.lib.saveAccum(this.ctx);
     return { k: ck.k, parts: ck.parts, width: this.width, height: this.height, accumulation: this.accumulation };
   }
+  // Order: update(scene) first (it resets the accumulation), then load(ckpt, scene): the scene is required, because
+  // its sampleCount must become k, or the next render() would restart the accumulation and drop the loaded samples.
   load(ckpt, scene) {
+    if (!scene) throw new Error('Renderer.load(ckpt, scene): the scene is required (its sampleCount continues at ckpt.k)');
     if (ckpt.width !== this.width || ckpt.height !== this.height) throw new Error('Renderer.load: checkpoint size differs');
     if (ckpt.accumulation && ckpt.accumulation !== this.accumulation) throw new Error('Renderer.load: accumulation mode differs');
     if (ckpt.frame) this.lib.loadAccum(this.ctx, -1, ckpt.frame, ckpt.k);
     else ckpt.parts.forEach((p, i) => this.lib.loadAccum(this.ctx, i, p, ckpt.k));
-    if (scene) scene.sampleCount = ckpt.k;  // the next render() draws sample k (its jitter and seed)
+    scene.sampleCount = ckpt.k;  // the next render() draws sample k (its jitter and seed)
   }
 
   readPixels() { return this.lib.readback(this.ctx, false).rgba; }

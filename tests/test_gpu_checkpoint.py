@@ -164,6 +164,55 @@ def test_load_rejects_bad_parts(gpu, fixtures):
         ctx.close()
 
 
+def test_load_rejects_mismatched_checkpoints(gpu, fixtures):
+    """Context.load refuses a checkpoint that does not fit: wrong array shape, part count, size,
+    accumulation mode or partition; and the C ABI refuses to use a multi-device frame whose parts are half loaded"""
+    sc = fixtures["scenes"]["C1"]
+    W, H, B = 24, 16, 3
+    inv, seeds = _sched(sc, W, H, 0, 2)
+    a = capi.Context(W, H, devices=[0, 0])
+    try:
+        a.set_scene_dict(sc)
+        a.render_schedule(inv, seeds, sc["eye"], B)
+        ck = a.save()
+    finally:
+        a.close()
+    assert ck["width"] == W and ck["height"] == H and ck["partition"] == [0, 1, capi.PART_TILES]
+    b = capi.Context(W, H, devices=[0, 0])
+    try:
+        b.set_scene_dict(sc)
+        bad_shape = dict(ck, parts=[p[:, :-1] for p in ck["parts"]])
+        with pytest.raises(capi.SailError, match="shape"):
+            b.load(bad_shape)
+        with pytest.raises(capi.SailError, match="parts"):
+            b.load(dict(ck, parts=ck["parts"][:1]))
+        with pytest.raises(capi.SailError, match="accum_mode"):
+            b.load(dict(ck, accum_mode=capi.ACCUM_MIX))
+        with pytest.raises(capi.SailError, match="partition"):
+            b.load(dict(ck, partition=[0, 1, capi.PART_SAMPLES]))
+        with pytest.raises(capi.SailError, match="width"):
+            b.load(dict(ck, width=W + 1))
+        # C ABI: part 0 alone leaves the frame half loaded -> every use is refused until part 1 arrives
+        p0 = np.ascontiguousarray(ck["parts"][0])
+        p1 = np.ascontiguousarray(ck["parts"][1])
+        assert b.lib.sail_load_accum(b.h, 0, capi._ptr(p0), ck["k"]) == 0
+        out = np.zeros((H, W, 4), np.float32)
+        assert b.lib.sail_read_accum(b.h, capi._ptr(out)) == -4
+        assert b.lib.sail_reduce(b.h, 0) == -4
+        assert b.lib.sail_load_accum(b.h, 1, capi._ptr(p1), ck["k"] + 1) == -1  # a different checkpoint's part
+        assert b.lib.sail_load_accum(b.h, 1, capi._ptr(p1), ck["k"]) == 0
+        got = b.read_accum()
+        b.load(ck)  # and through Context.load
+        assert bit_equal(b.read_accum(), got).all()
+        # sail_reset abandons a half-loaded checkpoint
+        assert b.lib.sail_load_accum(b.h, 1, capi._ptr(p1), ck["k"]) == 0
+        assert b.lib.sail_read_accum(b.h, capi._ptr(out)) == -4
+        b.reset()
+        assert b.lib.sail_read_accum(b.h, capi._ptr(out)) == 0
+    finally:
+        b.close()
+
+
 # ---- the sail_render queue (one-sample frames launched together) -------------------------------------------------
 @pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_render_queue_bit_exact_and_batched(gpu, fixtures, devices):

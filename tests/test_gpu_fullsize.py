@@ -27,8 +27,9 @@ def _bits_equal(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
 
 
-# (config, scene, W, H, bounces, spp) — BASELINE.json configs[1..3]
-FULL = [("C2", "C1", 1920, 1080, 8, 4), ("C3", "C3", 1920, 1080, 8, 2), ("C4", "C4", 3840, 2160, 12, 1)]
+# (config, scene, W, H, bounces, spp) — BASELINE.json configs[1..4] (C5: the converged Cornell render's 16 bounces)
+FULL = [("C2", "C1", 1920, 1080, 8, 4), ("C3", "C3", 1920, 1080, 8, 2), ("C4", "C4", 3840, 2160, 12, 1),
+        ("C5", "C1g", 1920, 1080, 16, 2)]
 
 
 @pytest.mark.parametrize("cfg,name,W,H,B,spp", FULL)
@@ -52,6 +53,49 @@ def test_full_frame_crops_match_oracle(frozen, cfg, name, W, H, B, spp):
         want = np.zeros((H, W, 4), np.float32)
         oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=want)
         assert _bits_equal(got[y0:y0 + c, x0:x0 + c], want[y0:y0 + c, x0:x0 + c]), (cfg, x0, y0)
+
+
+def test_c5_full_frame_sample_split_and_gaussian(frozen):
+    """BASELINE configs[4] at its full frame size: 1920x1080, 16 bounces, the sample split over 3 "devices" of one
+    GPU (the multi-device context's PART_SAMPLES path, summed in rank order) and the Gaussian r = 2, alpha = 2
+    reconstruction pass (window.glsl:26-44) over the reduced frame. The split frame counts every sample once and
+    equals the one-device frame to summation order; oracle crops of the uninterrupted frame match it to summation
+    order; the display pass equals the oracle filter of the same mean image bit for bit over the whole frame."""
+    sc = frozen["C1g"]
+    W, H, B, spp = 1920, 1080, 16, 5
+    flt = sc["filter"]
+    w16 = np.array(flt["weights64"], np.float32)
+    rx, ry = float(flt["radius"][0]), float(flt["radius"][1])
+    mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
+    inv, seeds = capi.schedule(mvp, W, H, 0, spp)
+    one = capi.Context(W, H)
+    one.set_scene_dict(sc)
+    one.render_schedule(inv, seeds, sc["eye"], B)
+    ref = one.read_accum()
+    one.close()
+    ctx = capi.Context(W, H, devices=[0, 0, 0])
+    try:
+        ctx.set_scene_dict(sc)
+        ctx.set_partition(0, 1, capi.PART_SAMPLES)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got = ctx.read_accum()
+        flt_out = ctx.filter(capi.FILTER_WINDOW, w16, rx, ry, 2.2)
+    finally:
+        ctx.close()
+    assert (got[..., 3] == spp).all(), "every pixel counts each sample once"
+    assert np.isfinite(got).all()
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-6)
+    masks = capi.plugin_masks(sc["plugins"])
+    c = 6
+    for x0, y0 in [(0, 0), (W - c, H - c), (W // 2, H // 2), (W // 5, 2 * H // 3)]:
+        want = np.zeros((H, W, 4), np.float32)
+        oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, crop=(x0, y0, c, c), accum=want)
+        assert _bits_equal(ref[y0:y0 + c, x0:x0 + c], want[y0:y0 + c, x0:x0 + c]), (x0, y0)
+        assert np.allclose(got[y0:y0 + c, x0:x0 + c], want[y0:y0 + c, x0:x0 + c], rtol=1e-5, atol=1e-6)
+    mean = got.copy()
+    mean[..., :3] = got[..., :3] / got[..., 3:4]
+    want_f = oracle.filter_image(mean, capi.FILTER_WINDOW, w16, rx, ry, 2.2)
+    assert _bits_equal(flt_out, want_f)
 
 
 def test_c2_eight_rank_split_equals_single_rank(frozen):

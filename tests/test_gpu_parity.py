@@ -608,3 +608,33 @@ def test_last_bounce_shortcut_edge_materials(gpu, fixtures, variant, B):
     assert same.all(), f"{variant}, {B} bounces: {int((~same).sum())} channels differ"
     if variant == "inf_kd":
         assert np.isnan(got[..., :3]).any() or np.isinf(got[..., :3]).any()
+
+
+# ---- the phase-timing build (the one instrumentation switch left in sail_trace.hip) ------------------------------
+@pytest.mark.parametrize("name,W,H,spp,B", [("C1", 40, 24, 3, 6), ("C3", 40, 24, 3, 5), ("C4", 40, 24, 2, 6)])
+def test_phase_timing_build_bit_exact(gpu, fixtures, monkeypatch, name, W, H, spp, B):
+    """libsail_hip_phase.so (-DSAIL_PHASE_TIMING=1, tools/phase_profile.py) renders the oracle's bits in all three
+    kernel families and its per-phase wave timers advance"""
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(capi.LIB_PATH), "libsail_hip_phase.so")
+    lib = capi.load(path)
+    lib.sail_phase_read.restype = ctypes.c_int
+    lib.sail_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    monkeypatch.setattr(capi, "_lib", lib)
+    buf = (ctypes.c_ulonglong * 8)()
+    assert lib.sail_phase_read(buf, 1) == 0
+    sc = fixtures["scenes"][name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    ctx = capi.Context(W, H)
+    try:
+        assert ctx.lib is lib
+        ctx.set_scene_dict(sc)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got = ctx.read_accum()
+    finally:
+        ctx.close()
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    assert bit_equal(got, want).all()
+    assert lib.sail_phase_read(buf, 0) == 0
+    assert buf[0] > 0 and buf[1] > 0  # sweep and hit-record phases were timed

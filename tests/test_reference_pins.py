@@ -205,7 +205,12 @@ def test_program_defines_match_kernel_and_oracle(fixtures, name):
             assert f32(v) in lits_k and f32(v) in lits_o, (col, v)
     # the object-space frame (OBJECT_SPACE_N/S/T = (0,1,0), (0,0,-1), (1,0,0))
     assert (d["OBJECT_SPACE_N"], d["OBJECT_SPACE_S"], d["OBJECT_SPACE_T"]) == ("vec3(0,1,0)", "vec3(0,0,-1)", "vec3(1,0,0)")
-    assert "v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, -1.0f), v3(1.0f, 0.0f, 0.0f)" in kern
+    # the kernel folds the frame's exact zero products into FMAs (W2L / L2W, sail_trace.hip), documented per row;
+    # the oracle keeps the reference's full dot products over the literal frame
+    assert "D V3 W2L(V3 v) {  // (dot(v, (0,0,-1)), dot(v, (1,0,0)), dot(v, (0,1,0)))" in kern
+    assert "D V3 L2W(V3 v) {  // (0,0,-1) v.x + (1,0,0) v.y + (0,1,0) v.z" in kern
+    for name, vec in (("OSN", "0.0f), F(1.0f), F(0.0f"), ("OSS", "0.0f), F(0.0f), F(-1.0f"), ("OST", "1.0f), F(0.0f), F(0.0f")):
+        assert "static const V3 %s = {F(%s)};" % (name, vec) in orc, name
 
 
 def _literal_map():
