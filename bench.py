@@ -259,6 +259,8 @@ def main():
                     help="skip the check of the reduced frame after the timed steps (counts + oracle crops)")
     ap.add_argument("--force-comm", action="store_true",
                     help="exercise the torch.distributed + RCCL reduce path even with one rank")
+    ap.add_argument("--debug", action="append", default=[], metavar="OPTION=VALUE",
+                    help="study: a sail_set_debug switch (include/sail_hip.h), e.g. 9=1 for the path-pool kernels")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -299,6 +301,9 @@ def main():
         ctx.set_debug(capi.DEBUG_FORCE_RCCL, 1)
     if args.wavefront:
         ctx.set_debug(capi.DEBUG_WAVEFRONT, 1)
+    debug = {int(k): int(v) for k, v in (d.split("=") for d in args.debug)}
+    for opt, val in debug.items():
+        ctx.set_debug(opt, val)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
     part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
@@ -386,7 +391,8 @@ def main():
                     "deterministic sample schedule",
             "config": {"workload": cfg["workload"] + ("_wavefront_split" if args.wavefront else ""), "width": W, "height": H, "bounces": B, "spp": spp,
                        "launch_spp": args.launch_spp, "partition": f"tiles64x{ngpu}",
-                       "processes": "one per GPU" if world > 1 else ("one (multi-device context)" if multi else "one"), "segments_per_step": W * H * spp * B},
+                       "processes": "one per GPU" if world > 1 else ("one (multi-device context)" if multi else "one"), "segments_per_step": W * H * spp * B,
+                       **({"debug": debug} if debug else {})},
             "roofline": {
                 # headline: the live-op model (ops some output reads: the last bounce's dead throughput update, next
                 # ray, BSDF sample and material weight left out), so skipped dead work is never credited

@@ -141,6 +141,8 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
+  int pathPool = 0;      // SAIL_DEBUG_PATH_POOL: the Cornell / room plugin sets run the path-pool kernels
+  bool lastPool = false; // the last trace launch ran a path-pool kernel (sail_kernel_name)
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
@@ -649,9 +651,12 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (G < 1) G = 1;
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
-    A.groupHome = SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
+    // the path-pool kernels finish samples out of order: every sample goes through the stage, even at G = 1
+    A.pathPool = c->pathPool && (A.kernelSet == SAIL_KSET_CORNELL || A.kernelSet == SAIL_KSET_ROOM) ? 1 : 0;
+    A.groupHome = !A.pathPool && SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
     A.stageStride = (long long)owned * 4096;
-    if (A.sampleGroups > 1) {
+    const bool staged = A.sampleGroups > 1 || A.pathPool;
+    if (staged) {
       const size_t need = (size_t)A.stageStride * (size_t)c->launchSpp * 3 * sizeof(float);
       if (need > c->stageBytes) {
         if (c->stage) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->stage)); c->stage = nullptr; }
@@ -684,11 +689,12 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       HIPCHK(c, sail_launch_wavefront(A, WS, c->stream));
     } else {
       HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
-      if (A.sampleGroups > 1) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
+      if (staged) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
     }
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending.emplace_back(e0, e1);
     c->lastGroups = A.sampleGroups;
+    c->lastPool = A.pathPool != 0;
     c->lastWavefront = wavefront;
     c->launches++;
     c->nominalSegments += (uint64_t)px * (uint64_t)nspp * (uint64_t)maxBounces;
@@ -853,7 +859,7 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
   // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
   if (c->lastWavefront) k = "sail_wf_*";
-  snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
+  snprintf(name, (size_t)len, "%s%s", k, c->lastPool ? "_pool" : (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }
 
@@ -1012,6 +1018,7 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
+    case SAIL_DEBUG_PATH_POOL: c->pathPool = value; break;
     case SAIL_DEBUG_GROUP_ROUNDS:
       if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
       c->flatGroupRounds = value;

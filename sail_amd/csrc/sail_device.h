@@ -70,7 +70,8 @@ struct SailTraceArgs {
   // sail_accum_kernel then adds the staged ones in sample order, so the sums are bit-identical to one workgroup
   // doing all samples
   int sampleGroups, groupSpp;
-  int groupHome;            // 1: group 0 accumulated its samples itself (SAIL_GROUP_HOME), the stage starts at groupSpp
+  int groupHome;            // 1: group 0 accumulated its samples itself (SAIL_GROUP_HOME_FOR), the stage starts at groupSpp
+  int pathPool;             // 1: the path-pool form of the Cornell / room kernel (traceTilePool; every sample staged)
   float* stage;             // three f32 planes per sample: stage[(3k + c) * stageStride + slot]
   long long stageStride;    // slots per sample = ownedTiles * 4096
 };

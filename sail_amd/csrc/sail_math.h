@@ -178,10 +178,8 @@ SM_D float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 // may also fold into the producing instruction's output clamp modifier): equal for every f32 x, NaN and signed
 // zeros included (tools/med3_probe.hip, all 2^32 inputs on an MI355X, profiles/r02_med3_probe.json)
 SM_D float clamp_(float x, float lo, float hi) {
-#if !defined(SAIL_NO_MED3)
   if (__builtin_constant_p(lo) && __builtin_constant_p(hi) && (lo == 0.0f || lo == -1.0f) && hi == 1.0f)
     return __builtin_amdgcn_fmed3f(x, lo, hi);
-#endif
   return fmin_(fmax_(x, lo), hi);
 }
 SM_D float fract_(float x) { return x - floorf(x); }
@@ -202,26 +200,10 @@ SM_D float sqrt01(float x) {
   if (__builtin_fmaf(-sup, s, x) > 0.0f) r = sup;
   return r;
 }
-// The general square root by the same core: the residual correction is exact wherever v_sqrt_f32 needs no
-// scaling -- +-0, NaN, +inf and every f32 >= 2^-96 (tools/sqrt01_probe.hip checks all of them against the IEEE
-// lowering) -- and the rest (tiny positives, subnormals, negatives) takes the compiler's IEEE sqrt behind a real
-// branch (an empty volatile asm keeps it from being if-converted into every call). Exact on all 2^32 inputs
-// (profiles/r03_sqrt_probe.json) but measured C2 +0.1 %, C3 -0.5 %, C4 -0.6 %, so SAIL_SQRT_CORE defaults to 0 (IEEE).
-#ifndef SAIL_SQRT_CORE
-#define SAIL_SQRT_CORE 0
-#endif
-SM_D float sqrtg(float x) {
-#if SAIL_SQRT_CORE
-  if (__builtin_expect(x < 0x1p-96f && x != 0.0f, 0)) {
-    float xx = x;
-    __asm__ volatile("" : "+v"(xx));
-    return __builtin_sqrtf(xx);
-  }
-  return sqrt01(x);
-#else
-  return __builtin_sqrtf(x);
-#endif
-}
+// The general square root is the IEEE one. (The same residual-corrected core with the IEEE root behind a branch for
+// tiny, subnormal and negative arguments was exact on all 2^32 inputs, profiles/r03_sqrt_probe.json, but measured
+// C2 +0.1 %, C3 -0.5 %, C4 -0.6 %.)
+SM_D float sqrtg(float x) { return __builtin_sqrtf(x); }
 SM_D float sqrtf_(float x) { return sqrtg(x); }
 // GLSL division a / b := a * RN(1/b) (the reciprocal-multiply form shader compilers emit, with the reciprocal
 // correctly rounded; oracle/ref_math.h div_s). RN(1/b) = one Newton step from the hardware reciprocal, equal to
