@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <math.h>
+#include <algorithm>
 #include <cmath>
 #include <stdarg.h>
 #include <stdio.h>
@@ -228,6 +229,10 @@ int kernelSetFor(const sail_ctx* c) {
   return SAIL_KSET_GENERIC;
 }
 
+// the sample-group / path-pool stage's cap (12 B per owned pixel per staged sample): 8 GiB
+constexpr size_t kStageCapBytes = (size_t)8 << 30;
+int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY);
+int ownedTilesOnly(const sail_ctx* c) { int tx, ty; return ownedTiles(c, &tx, &ty); }
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
   const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
   *tilesX = tx; *tilesY = ty;
@@ -604,8 +609,15 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   c->samplesPos += count;
   HIPCHK(c, hipMemcpyAsync(dev, src, sizeof(SailSample) * count, hipMemcpyHostToDevice, c->stream));
   const long long px = ownedPixels(c);
-  for (int s0 = 0; s0 < count; s0 += c->launchSpp) {
-    const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
+  // The stage holds 12 B per owned pixel per staged sample. It is capped (kStageCapBytes): the path-pool kernels, which
+  // stage every sample, split a longer launch into launches of at most stageSpp samples; the grouped kernels fall back
+  // to one workgroup per block (no stage) when a launch would need more.
+  const long long stageStride = (long long)ownedTilesOnly(c) * 4096;
+  const int stageSpp = (int)std::max<long long>(1, (long long)(kStageCapBytes / ((size_t)stageStride * 12)));
+  const bool poolSet = c->pathPool && (kernelSetFor(c) == SAIL_KSET_CORNELL || kernelSetFor(c) == SAIL_KSET_ROOM);
+  const int perLaunch = poolSet ? std::min(c->launchSpp, stageSpp) : c->launchSpp;
+  for (int s0 = 0; s0 < count; s0 += perLaunch) {
+    const int nspp = (count - s0) < perLaunch ? (count - s0) : perLaunch;
     SailTraceArgs A;
     memset(&A, 0, sizeof A);
     A.prims = c->prims; A.typeMasks = reinterpret_cast<const unsigned long long*>(c->prims + c->n);
@@ -649,15 +661,16 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     }
     if (G > nspp) G = nspp;
     if (G < 1) G = 1;
+    if (nspp > stageSpp && !poolSet) G = 1;  // the stage would pass its cap
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
     // the path-pool kernels finish samples out of order: every sample goes through the stage, even at G = 1
-    A.pathPool = c->pathPool && (A.kernelSet == SAIL_KSET_CORNELL || A.kernelSet == SAIL_KSET_ROOM) ? 1 : 0;
+    A.pathPool = poolSet ? 1 : 0;
     A.groupHome = !A.pathPool && SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
-    A.stageStride = (long long)owned * 4096;
+    A.stageStride = stageStride;
     const bool staged = A.sampleGroups > 1 || A.pathPool;
-    if (staged) {
-      const size_t need = (size_t)A.stageStride * (size_t)c->launchSpp * 3 * sizeof(float);
+    if (staged) {  // sized for this launch's samples (it grows to the largest launch seen)
+      const size_t need = (size_t)A.stageStride * (size_t)nspp * 3 * sizeof(float);
       if (need > c->stageBytes) {
         if (c->stage) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->stage)); c->stage = nullptr; }
         c->stageBytes = 0;

@@ -32,7 +32,8 @@ def main():
         W, H, B, spp = (3840, 2160, 12, 8) if name == "C4" else (1920, 1080, 8, 64)
         mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
         inv, seeds = capi.schedule(mvp, W, H, 0, spp)
-        ctx = capi.Context(W, H)
+        dbg = {int(k): int(v) for k, v in (o.split("=") for o in os.environ.get("PHASE_DEBUG", "").split(",") if o)}
+        ctx = capi.Context(W, H, debug=dbg)
         ctx.set_scene_dict(sc)
         lib.sail_phase_read(buf, 1)
         ctx.render_schedule(inv, seeds, sc["eye"], B)

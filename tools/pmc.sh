@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" -d $ROOT/${PMC_OUT:-gpurun_out/pmc}/$name -o run --output-format csv -- \
-    python3 $ROOT/bench.py --config ${PMC_CONFIG:-C2} --steps 1 --warmup 0 --spp ${PMC_SPP:-64} --no-cpu-baseline > $ROOT/${PMC_OUT:-gpurun_out/pmc}/$name.log 2>&1
+    python3 $ROOT/bench.py --config ${PMC_CONFIG:-C2} --steps 1 --warmup 0 --spp ${PMC_SPP:-64} --no-cpu-baseline ${PMC_BENCH_ARGS:-} > $ROOT/${PMC_OUT:-gpurun_out/pmc}/$name.log 2>&1
 }
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1

@@ -14,14 +14,14 @@ sys.path.insert(0, ROOT)
 from sail_amd import capi  # noqa: E402
 
 
-def run(path, sc, W, H, B, spp, launch, reps):
+def run(path, sc, W, H, B, spp, launch, reps, debug=None):
     lib = capi.load(path)
     saved = capi._lib
     capi._lib = lib
     try:
         mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
         inv, seeds = capi.schedule(mvp, W, H, 0, spp)
-        ctx = capi.Context(W, H)
+        ctx = capi.Context(W, H, debug=debug)
         ctx.set_scene_dict(sc)
         ctx.set_launch_samples(launch)
         ctx.render_schedule(inv, seeds, sc["eye"], B)  # warm-up
@@ -47,20 +47,31 @@ def run(path, sc, W, H, B, spp, launch, reps):
 
 
 def main():
+    """variant_bench.py SCENE [NAME=LIB[:OPT=VAL,...] ...]: each spec is a library (a path, or "main" for
+    sail_amd/lib/libsail_hip.so) with sail_set_debug switches; without specs, every sail_amd/lib/variants/*.so."""
     scene = sys.argv[1] if len(sys.argv) > 1 else "C1"
     W, H, B, spp = (3840, 2160, 12, 8) if scene == "C4" else (1920, 1080, 8, 128)
     with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
         sc = json.load(f)[scene]
-    paths = sorted(glob.glob(os.path.join(ROOT, "sail_amd", "lib", "variants", "libsail_hip_*.so")))
+    specs = []
+    for a in sys.argv[2:]:
+        name, rest = a.split("=", 1)
+        lib, _, opts = rest.partition(":")
+        lib = capi.LIB_PATH if lib == "main" else os.path.join(ROOT, lib)
+        dbg = {int(k): int(v) for k, v in (o.split("=") for o in opts.split(",") if o)}
+        specs.append((name, lib, dbg))
+    if not specs:
+        specs = [(os.path.basename(p), p, None)
+                 for p in sorted(glob.glob(os.path.join(ROOT, "sail_amd", "lib", "variants", "libsail_hip_*.so")))]
     rounds = int(os.environ.get("VARIANT_ROUNDS", "2"))  # ABCD ABCD: clock drift shows as a spread, not a bias
     ref = None
-    for p in paths * rounds:
-        dt, ms, acc, div_bad = run(p, sc, W, H, B, spp, 32, 3)
+    for name, p, dbg in specs * rounds:
+        dt, ms, acc, div_bad = run(p, sc, W, H, B, spp, 32, 3, dbg)
         same = ref is None or np.array_equal(acc.view(np.uint32), ref.view(np.uint32))
         if ref is None:
             ref = acc
         segs = W * H * spp * B
-        print(json.dumps({"variant": os.path.basename(p), "scene": scene, "s": round(dt, 4), "ms_per_launch": round(ms, 3),
+        print(json.dumps({"variant": name, "scene": scene, "debug": dbg, "s": round(dt, 4), "ms_per_launch": round(ms, 3),
                           "Gseg_per_s": round(segs / dt / 1e9, 3), "bit_identical": bool(same), "divide_mismatches": div_bad}), flush=True)
 
 
