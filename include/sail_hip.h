@@ -116,10 +116,7 @@ enum sail_debug_option {
   /* > 0: residency rounds of workgroups queued per launch when sizing the sample groups, flat kernels [36] and the
    * pre-cull kernel [64] (SAIL_DEBUG_SAMPLE_GROUPS overrides both) */
   SAIL_DEBUG_GROUP_ROUNDS = 7,
-  SAIL_DEBUG_CULL_GROUP_ROUNDS = 8,
-  /* 1: the Cornell and room plugin sets run the path-pool kernels (class-uniform waves, every sample staged); 0: the
-   * compacting kernels [0] */
-  SAIL_DEBUG_PATH_POOL = 9
+  SAIL_DEBUG_CULL_GROUP_ROUNDS = 8
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 

@@ -142,8 +142,6 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int pathPool = 0;      // SAIL_DEBUG_PATH_POOL: the Cornell / room plugin sets run the path-pool kernels
-  bool lastPool = false; // the last trace launch ran a path-pool kernel (sail_kernel_name)
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
@@ -229,10 +227,8 @@ int kernelSetFor(const sail_ctx* c) {
   return SAIL_KSET_GENERIC;
 }
 
-// the sample-group / path-pool stage's cap (12 B per owned pixel per staged sample): 8 GiB
+// the sample-group stage's cap (12 B per owned pixel per staged sample): 8 GiB
 constexpr size_t kStageCapBytes = (size_t)8 << 30;
-int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY);
-int ownedTilesOnly(const sail_ctx* c) { int tx, ty; return ownedTiles(c, &tx, &ty); }
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
   const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
   *tilesX = tx; *tilesY = ty;
@@ -609,15 +605,12 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   c->samplesPos += count;
   HIPCHK(c, hipMemcpyAsync(dev, src, sizeof(SailSample) * count, hipMemcpyHostToDevice, c->stream));
   const long long px = ownedPixels(c);
-  // The stage holds 12 B per owned pixel per staged sample. It is capped (kStageCapBytes): the path-pool kernels, which
-  // stage every sample, split a longer launch into launches of at most stageSpp samples; the grouped kernels fall back
-  // to one workgroup per block (no stage) when a launch would need more.
-  const long long stageStride = (long long)ownedTilesOnly(c) * 4096;
+  // The stage holds 12 B per owned pixel per staged sample. It is capped (kStageCapBytes): a launch that would need
+  // more runs one workgroup per block (no stage).
+  const long long stageStride = (long long)owned * 4096;
   const int stageSpp = (int)std::max<long long>(1, (long long)(kStageCapBytes / ((size_t)stageStride * 12)));
-  const bool poolSet = c->pathPool && (kernelSetFor(c) == SAIL_KSET_CORNELL || kernelSetFor(c) == SAIL_KSET_ROOM);
-  const int perLaunch = poolSet ? std::min(c->launchSpp, stageSpp) : c->launchSpp;
-  for (int s0 = 0; s0 < count; s0 += perLaunch) {
-    const int nspp = (count - s0) < perLaunch ? (count - s0) : perLaunch;
+  for (int s0 = 0; s0 < count; s0 += c->launchSpp) {
+    const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
     SailTraceArgs A;
     memset(&A, 0, sizeof A);
     A.prims = c->prims; A.typeMasks = reinterpret_cast<const unsigned long long*>(c->prims + c->n);
@@ -661,14 +654,12 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     }
     if (G > nspp) G = nspp;
     if (G < 1) G = 1;
-    if (nspp > stageSpp && !poolSet) G = 1;  // the stage would pass its cap
+    if (nspp > stageSpp) G = 1;  // the stage would pass its cap
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
-    // the path-pool kernels finish samples out of order: every sample goes through the stage, even at G = 1
-    A.pathPool = poolSet ? 1 : 0;
-    A.groupHome = !A.pathPool && SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
+    A.groupHome = SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
     A.stageStride = stageStride;
-    const bool staged = A.sampleGroups > 1 || A.pathPool;
+    const bool staged = A.sampleGroups > 1;
     if (staged) {  // sized for this launch's samples (it grows to the largest launch seen)
       const size_t need = (size_t)A.stageStride * (size_t)nspp * 3 * sizeof(float);
       if (need > c->stageBytes) {
@@ -707,7 +698,6 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending.emplace_back(e0, e1);
     c->lastGroups = A.sampleGroups;
-    c->lastPool = A.pathPool != 0;
     c->lastWavefront = wavefront;
     c->launches++;
     c->nominalSegments += (uint64_t)px * (uint64_t)nspp * (uint64_t)maxBounces;
@@ -872,7 +862,7 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
   // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
   if (c->lastWavefront) k = "sail_wf_*";
-  snprintf(name, (size_t)len, "%s%s", k, c->lastPool ? "_pool" : (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
+  snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }
 
@@ -1031,7 +1021,6 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
-    case SAIL_DEBUG_PATH_POOL: c->pathPool = value; break;
     case SAIL_DEBUG_GROUP_ROUNDS:
       if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
       c->flatGroupRounds = value;

@@ -71,7 +71,6 @@ struct SailTraceArgs {
   // doing all samples
   int sampleGroups, groupSpp;
   int groupHome;            // 1: group 0 accumulated its samples itself (SAIL_GROUP_HOME_FOR), the stage starts at groupSpp
-  int pathPool;             // 1: the path-pool form of the Cornell / room kernel (traceTilePool; every sample staged)
   float* stage;             // three f32 planes per sample: stage[(3k + c) * stageStride + slot]
   long long stageStride;    // slots per sample = ownedTiles * 4096
 };

@@ -1939,293 +1939,6 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
   }
 }
-// ---- path pool: class-uniform waves for the flat kernels (round 4) ------------------------------------------------
-// The compacting kernel sorts the workgroup's 256 paths every bounce, but a sorted range of 256 paths over six classes
-// (C3: walls, four spheres of four materials, the light) still leaves two of its four waves mixed: every class whose
-// paths straddle a wave boundary, or are too few to fill one, runs its hit record and material branch once per wave it
-// touches. Deleting the minority lanes' shading bounded that cost at +26 % on C3 and +8 % on C2
-// (profiles/r03_majority_probe.jsonl). Larger sort pools did not collect it (a wider barrier, more spills).
-// Here a workgroup keeps a pool of P > 256 paths in LDS (64 B records) and shades, each round, only whole waves of one
-// class: a class's paths wait in the pool until they fill 64 lanes (or the pool is full and nothing fills, or no new
-// work is left, when leftovers are shaded as before). Every lane that shaded a path sweeps its next ray at once;
-// a lane whose path ended, or that got no path this round, takes a new one (the next pixel-sample of the
-// workgroup's block, sample-major) into a free slot. A path's arithmetic is the same as in traceTileCompact (hash
-// seed, shading, next ray, depth), and each finished sample's radiance goes to the stage; sail_accum_kernel adds the
-// stage in sample order, so the frame is bit-identical to the compacting kernels'.
-// Per round: (1) slot and work allocation (one LDS atomic per wave), sweep; (2) the record and its class count (LDS
-// atomics), plus the counts of the waiting records; barrier; (3) every wave scans the 64 class counts and places each
-// path: the class's full waves first, promoted leftovers after them, the rest stays waiting; barrier; (4) lane i
-// shades the path in slot perm[i]. Two barriers per round, as the room kernel's two-barrier sort.
-template <uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int P, int MINSHADE>
-__device__ __forceinline__ void traceTilePool(const SailTraceArgs& A) {
-  constexpr int NT = 256, kKeys = 64, kWait = 0x10000;
-  static_assert(P >= NT && P <= 2 * NT, "pool slots li and li + 256 are visited by lane li");
-  // path record, four float4 per slot: ray o + d.x | d.yz + throughput.xy | throughput.z, distance, pixel | row << 8,
-  // klocal | depth << 20 | radiance, key (+ kWait while the path waits for its class)
-  __shared__ float4 sRec[4][P];
-  __shared__ int sPerm[NT];
-  __shared__ int sCnt[2][kKeys];
-  __shared__ int sQ[2];  // [0] next work item, [1] next never-used slot
-  const TileWork tw = tileWork<true, NT>(A);
-  if (tw.ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
-  const int sub = tw.sub;
-  const int tile = A.rank + tw.ownedTile * A.world;
-  const int tx = tile % A.tilesX, ty = tile / A.tilesX;
-  const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
-  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * 16;
-  // the block's pixels inside the frame (a ragged tile's blocks may hold fewer, or none)
-  const int vw = A.W - x0 < 16 ? (A.W - x0 > 0 ? A.W - x0 : 0) : 16;
-  const int vh = A.H - y0 < 16 ? (A.H - y0 > 0 ? A.H - y0 : 0) : 16;
-  const int nValid = vw * vh;
-  const int qTotal = nValid * (tw.kEnd - tw.kBeg);
-
-  Ctx c;
-  c.tp = A.texparams; c.lt = A.lights; c.lightObjRow = A.lightObjRow; c.typeMasks = A.typeMasks;
-  c.prims = A.prims;
-  c.cprims = A.prims;
-  c.tpl = A.texparams;
-  c.rowCopy = false;
-  c.tpCopy = false;
-  c.n = A.n; c.tn = A.tn; c.ln = A.ln;
-  c.matMask = A.matMask; c.texMask = A.texMask; c.lightMask = A.lightMask;
-  c.fcx = 0.0f; c.fcy = 0.0f;
-  c.shadowAnyHit = A.shadowAnyHit;
-  c.cullPrims = 0;
-  c.cullFma = 0;
-  c.cullPrimary = A.cullPrimary;
-  c.kShapes = KS; c.kMats = KM; c.kTex = KT; c.kLights = KL;
-
-  for (int i = li; i < P; i += NT) sRec[3][i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // no record waits
-  if (li < 2 * kKeys) sCnt[li / kKeys][li % kKeys] = 0;
-  if (li < 2) sQ[li] = 0;
-  __syncthreads();
-  const bool byPrim = A.n < kKeys;
-  const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
-  const float fW = (float)A.W, fH = (float)A.H;
-  int mySlot = -1;       // the slot of the path this lane carries (or refills)
-  bool have = false;     // the lane carries a path whose next sweep is due
-  bool qDone = qTotal == 0;
-  Ray ray;
-  ray.o = v3s(0.0f); ray.d = v3s(0.0f); ray.rx = ray.ry = ray.rz = 0.0f;
-  V3 f = v3s(1.0f), e = v3s(0.0f);
-  int pixel = 0, klocal = 0, depth = 0;
-  unsigned segs = 0;
-  int ph = 0;
-  if (A.maxBounces < 1) {  // uniform: no bounce, every sample's radiance is 0 (and nothing is swept)
-    for (int q = li; q < qTotal; q += NT) {
-      const int kl = q / nValid, p = q - kl * nValid, py = p / vw;
-      stageSample<NT>(A, tw.kBeg + kl, tw.bid, py * 16 + (p - py * vw), v3s(0.0f));
-    }
-    return;
-  }
-  PhaseClock pc;
-#if SAIL_PHASE_TIMING
-  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
-  pc.t = __builtin_amdgcn_s_memtime();
-#endif
-  // a finished sample: its radiance into the stage (planes of sample kBeg + klocal, the block's slot order)
-  auto finish = [&]() {
-    stageSample<NT>(A, tw.kBeg + klocal, tw.bid, pixel, e);
-    have = false;
-  };
-  for (;;) {
-    // ---- (1) a free slot for a lane without one, then new work and the sweep, until every lane of the wave carries
-    // a swept path or no slot / no work is left (a path that leaves the scene finishes and its lane refills)
-    {
-      const bool needSlot = !have && mySlot < 0 && !qDone;
-      const unsigned long long m = __builtin_amdgcn_ballot_w64(needSlot);
-      if (m != 0ull) {
-        const int first = __builtin_ctzll(m);
-        int base = 0;
-        if (lane == first) base = atomicAdd(&sQ[1], __popcll(m));
-        base = __builtin_amdgcn_readlane(base, first);
-        if (needSlot) {
-          const int s = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          mySlot = s < P ? s : -1;
-        }
-      }
-    }
-    bool swept = false;
-    Sweep sw;
-    sw.best = kMaxDistance; sw.bi = -1; sw.bhl = v3s(0.0f);
-    int key = 0;
-    for (;;) {
-      const bool needWork = !have && mySlot >= 0 && !qDone;
-      const unsigned long long m = __builtin_amdgcn_ballot_w64(needWork);
-      if (m != 0ull) {
-        const int first = __builtin_ctzll(m);
-        int base = 0;
-        if (lane == first) base = atomicAdd(&sQ[0], __popcll(m));
-        base = __builtin_amdgcn_readlane(base, first);
-        if (needWork) {
-          const int q = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-          if (q >= qTotal) {
-            qDone = true;
-          } else {  // pixel-sample q (sample-major): a primary ray as traceTileCompact builds it
-            klocal = q / nValid;
-            const int p = q - klocal * nValid, py = p / vw, px = p - py * vw;
-            pixel = py * 16 + px;
-            const SailSample& S = A.samples[tw.kBeg + klocal];
-            const float s = ((float)(x0 + px) + 0.5f) / fW, t = ((float)(y0 + py) + 0.5f) / fH;
-            const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
-            const V3 d2 = v3(S.d[2][0], S.d[2][1], S.d[2][2]), d3 = v3(S.d[3][0], S.d[3][1], S.d[3][2]);
-            ray = mkRay(eye, (s + t <= 1.0f) ? (d0 + (d2 - d0) * s + (d1 - d0) * t)
-                                             : (d3 + (d1 - d3) * (1.0f - s) + (d2 - d3) * (1.0f - t)));
-            f = v3s(1.0f);
-            e = v3s(0.0f);
-            depth = 1;
-            have = true;
-          }
-        }
-      }
-      const bool doSweep = have && !swept;
-      if (__builtin_amdgcn_ballot_w64(doSweep) == 0ull) break;
-      if (doSweep) {
-        segs++;
-        sw = sweepRay(c, ray, depth == 1);
-        if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
-          if (depth == 1 && (A.aovN || A.aovP) && tw.kBeg + klocal == A.spp - 1) {  // fstrace.glsl:15-16, n = p = 0
-            const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
-            const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
-            if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
-            if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
-          }
-          finish();
-        } else {
-          if (byPrim) {
-            key = 1 + sw.bi;
-          } else {
-            const SailPrim& pr = PRIM(c, sw.bi);
-            int mc = matCat(pr);
-            mc = (mc >= 0 && mc < 5) ? mc : 0;
-            key = 1 + mc * 10 + pr.type;
-          }
-          swept = true;
-        }
-      }
-    }
-    PHASE_MARK(pc, 0);
-    // ---- (2) the record of each swept path and its class count; the owners of waiting records count them too
-    int rank = 0;
-    if (swept) {
-      sRec[0][mySlot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
-      sRec[1][mySlot] = make_float4(ray.d.y, ray.d.z, f.x, f.y);
-      sRec[2][mySlot] = make_float4(f.z, sw.best, __int_as_float(pixel | (sw.bi << 8)), __int_as_float(klocal | (depth << 20)));
-      sRec[3][mySlot] = make_float4(e.x, e.y, e.z, __int_as_float(key));
-      rank = atomicAdd(&sCnt[ph][key], 1);
-    }
-    int wKey[2] = {0, 0}, wRank[2] = {-1, -1};
-#pragma unroll
-    for (int v = 0; v < 2; v++) {
-      const int s = li + v * NT;
-      if (s < P) {
-        const int w = __float_as_int(sRec[3][s].w);
-        if (w & kWait) { wKey[v] = w & 0xffff; wRank[v] = atomicAdd(&sCnt[ph][wKey[v]], 1); }
-      }
-    }
-    __syncthreads();
-    // ---- (3) every wave places the paths: per class, its full waves of 64 first (in class order, at most 256 lanes),
-    // then -- when the pool is full and fewer than MINSHADE lanes would shade, or no work is left -- the leftovers
-    const int cnt = sCnt[ph][lane];
-    const int live = __builtin_amdgcn_readlane(waveScanIncl(cnt), 63);
-    if (live == 0) break;  // uniform: no path is left and no work
-    const bool noWork = __builtin_amdgcn_readfirstlane(sQ[0]) >= qTotal;
-    const bool poolFull = __builtin_amdgcn_readfirstlane(sQ[1]) >= P;
-    const int full = cnt & ~63;
-    const int fullIncl = waveScanIncl(full);
-    const int fStart = fullIncl - full;
-    const int fShade = full < NT - fStart ? full : (NT - fStart > 0 ? NT - fStart : 0);
-    const int nFull = __builtin_amdgcn_readlane(waveScanIncl(fShade), 63);
-    const bool promote = nFull < MINSHADE && (poolFull || noWork);
-    const int left = promote ? cnt - fShade : 0;
-    const int leftIncl = waveScanIncl(left);
-    const int lStart = nFull + leftIncl - left;
-    const int lShade = left < NT - lStart ? left : (NT - lStart > 0 ? NT - lStart : 0);
-    const int nShade = nFull + __builtin_amdgcn_readlane(waveScanIncl(lShade), 63);
-    const int selA = fStart | (fShade << 16), selB = lStart | (lShade << 16);
-    // position of the path of class k with rank r among the class's paths, or -1 (it waits)
-    auto place = [&](int k, int r) -> int {
-      const int a = __shfl(selA, k, 64), b = __shfl(selB, k, 64);
-      const int fs = a & 0xffff, fn = a >> 16, ls = b & 0xffff, ln = b >> 16;
-      if (r < fn) return fs + r;
-      if (r - fn < ln) return ls + (r - fn);
-      return -1;
-    };
-    {
-      const int pos = place(key, rank);
-      if (swept) {
-        if (pos >= 0) sPerm[pos] = mySlot;
-        else reinterpret_cast<int*>(&sRec[3][mySlot])[3] = key | kWait;
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 2; v++) {
-      const int pos = place(wKey[v], wRank[v]);
-      if (wRank[v] >= 0 && pos >= 0) {
-        const int s = li + v * NT;
-        sPerm[pos] = s;
-        reinterpret_cast<int*>(&sRec[3][s])[3] = wKey[v];  // no longer waiting
-      }
-    }
-    __syncthreads();
-    if (wave == 0) sCnt[ph][lane] = 0;  // read by every wave before the barrier; counted into again two rounds on
-    ph ^= 1;
-    PHASE_MARK(pc, 7);
-    // ---- (4) lane i shades the path in slot perm[i]: the hit record and the bounce, as traceTileCompact
-    if (li < nShade) {
-      mySlot = sPerm[li];
-      const float4 q0 = sRec[0][mySlot], q1 = sRec[1][mySlot], q2 = sRec[2][mySlot], q3 = sRec[3][mySlot];
-      ray.o = v3(q0.x, q0.y, q0.z);
-      ray.d = v3(q0.w, q1.x, q1.y);
-      ray.rx = ray.ry = ray.rz = 0.0f;  // not used past the sweep: the next ray is rebuilt by mkRay
-      f = v3(q1.z, q1.w, q2.x);
-      sw.best = q2.y;
-      const int w0 = __float_as_int(q2.z), w1 = __float_as_int(q2.w);
-      pixel = w0 & 255;
-      sw.bi = w0 >> 8;
-      sw.bhl = v3s(0.0f);  // recomputed by hitRecord<true>
-      klocal = w1 & 0xfffff;
-      depth = w1 >> 20;
-      e = v3(q3.x, q3.y, q3.z);
-      const int keyG = __float_as_int(q3.w) & 0xffff;
-      {  // a promoted (mixed) wave runs several branches: raise its issue priority, as traceTileCompact
-        const int k0 = __builtin_amdgcn_readfirstlane(keyG);
-        const bool mixedW = __builtin_amdgcn_ballot_w64(keyG != k0) != 0ull;
-        if (mixedW) __builtin_amdgcn_s_setprio(kPrioMixed);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-      c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
-      c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
-      const Hit ins = hitRecordU<true>(c, ray, sw);
-      PHASE_MARK(pc, 1);
-      const int kg = tw.kBeg + klocal;
-      if (depth == 1 && (A.aovN || A.aovP) && kg == A.spp - 1) {
-        const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
-        const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
-        if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
-        if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
-      }
-      const float seed = A.samples[kg].seed + (float)depth;
-      if (!(depth == A.maxBounces && shadeLast(c, ins, seed, f, e))) shadeBounce(c, ins, ray, seed, f, e, pc);
-      have = true;
-      if (depth >= A.maxBounces) finish();
-      else depth++;
-    } else {
-      mySlot = -1;
-      have = false;
-    }
-  }
-#if SAIL_PHASE_TIMING
-  if (lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
-#endif
-  if (A.segCounter) {
-    unsigned long long v = segs;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) atomicAdd(&A.segCounter[(blockIdx.x * 4u + (unsigned)wave) % SAIL_SEG_SLOTS], v);
-  }
-}
-
 // Path compaction (traceTileCompact) in every plugin-set kernel: C2 +6 %, C3 +12 %, C4 +10 % (measured;
 // earlier builds with more live state lost to spills in the flat kernels).
 // Each plugin set has an ungrouped kernel (one workgroup per 16 x NT/16 block, every sample) and a _grouped one
@@ -2253,25 +1966,6 @@ SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_CORNELL_WAVES, false, SAIL_KS
 #define SAIL_ROOM_GROUP_NT 256
 SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_ROOM_WAVES, false, SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS,
                    SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT)
-// the path-pool forms (traceTilePool) of the Cornell and room kernels: pool slots within the LDS the occupancy allows
-// (8 waves: 20 KB per workgroup, 7 waves: 22.8 KB)
-#ifndef SAIL_POOL_CORNELL_P
-#define SAIL_POOL_CORNELL_P 288
-#endif
-#ifndef SAIL_POOL_ROOM_P
-#define SAIL_POOL_ROOM_P 320
-#endif
-#ifndef SAIL_POOL_MINSHADE
-#define SAIL_POOL_MINSHADE 1
-#endif
-extern "C" __global__ void __launch_bounds__(256, SAIL_CORNELL_WAVES) sail_trace_kernel_cornell_pool(SailTraceArgs A) {
-  traceTilePool<SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS, SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS,
-                SAIL_POOL_CORNELL_P, SAIL_POOL_MINSHADE>(A);
-}
-extern "C" __global__ void __launch_bounds__(256, SAIL_ROOM_WAVES) sail_trace_kernel_room_pool(SailTraceArgs A) {
-  traceTilePool<SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS, SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_POOL_ROOM_P,
-                SAIL_POOL_MINSHADE>(A);
-}
 // the pre-cull kernel serves scenes with many primitives (C4); 1,024-thread workgroups (16 x 64 strips)
 #define SAIL_CULL_WAVES 8
 #define SAIL_CULL_NT 1024
@@ -2714,11 +2408,7 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s) 
     if (g) hipLaunchKernelGGL(k##_grouped, dim3(blocks * 256 / (gnt)), dim3(gnt), 0, s, A);     \
     else hipLaunchKernelGGL(k, dim3(blocks * 256 / (nt)), dim3(nt), 0, s, A);                     \
   } while (0)
-  if (A.pathPool && A.kernelSet == SAIL_KSET_CORNELL)
-    hipLaunchKernelGGL(sail_trace_kernel_cornell_pool, dim3(blocks), dim3(256), 0, s, A);
-  else if (A.pathPool && A.kernelSet == SAIL_KSET_ROOM)
-    hipLaunchKernelGGL(sail_trace_kernel_room_pool, dim3(blocks), dim3(256), 0, s, A);
-  else if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT);
+  if (A.kernelSet == SAIL_KSET_CORNELL) SAIL_LAUNCH_NT(sail_trace_kernel_cornell, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT);
   else if (A.kernelSet == SAIL_KSET_ROOM) SAIL_LAUNCH_NT(sail_trace_kernel_room, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT);
   else if (A.cullPrims) SAIL_LAUNCH_NT(sail_trace_kernel_cull, SAIL_CULL_NT, SAIL_CULL_GROUP_NT);
   else SAIL_LAUNCH(sail_trace_kernel);
