@@ -13,9 +13,12 @@ $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_trace.hip -o build/sail_trace.o
 $HIPCC $COMMON --offload-arch=$ARCH -DSAIL_PHASE_TIMING=1 -c csrc/sail_trace.hip -o build/sail_trace_phase.o &
 $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_capi.cpp -o build/sail_capi.o &
 $HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_hostmath.cpp -o build/sail_hostmath.o &
+# the per-plugin-set kernels compiled at run time (sail_jit.cpp) carry the kernel sources in the library
+python3 gen_jit_src.py build/sail_jit_src.cpp csrc
+$HIPCC $COMMON --offload-arch=$ARCH -c csrc/sail_jit.cpp -o build/sail_jit.o &
+$HIPCC $COMMON --offload-arch=$ARCH -c build/sail_jit_src.cpp -o build/sail_jit_src.o &
 wait
-for o in build/sail_trace.o build/sail_trace_phase.o build/sail_capi.o build/sail_hostmath.o; do [ -s $o ] || { echo "missing $o"; exit 1; }; done
-$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o build/sail_capi.o build/sail_hostmath.o \
-  -o lib/libsail_hip.so -ldl
-$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace_phase.o build/sail_capi.o build/sail_hostmath.o \
-  -o lib/libsail_hip_phase.so -ldl
+HOST="build/sail_capi.o build/sail_hostmath.o build/sail_jit.o build/sail_jit_src.o"
+for o in build/sail_trace.o build/sail_trace_phase.o $HOST; do [ -s $o ] || { echo "missing $o"; exit 1; }; done
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o $HOST -o lib/libsail_hip.so -ldl -lhiprtc
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace_phase.o $HOST -o lib/libsail_hip_phase.so -ldl -lhiprtc

@@ -27,6 +27,7 @@ DEBUG_CULL_MIN_PRIMS, DEBUG_FORCE_GENERIC, DEBUG_CULL_FMA, DEBUG_SAMPLE_GROUPS, 
 DEBUG_WAVEFRONT = 6
 DEBUG_GROUP_ROUNDS = 7
 DEBUG_CULL_GROUP_ROUNDS = 8
+DEBUG_JIT = 9
 # applied to every Context at creation (tests set entries with monkeypatch.setitem)
 DEBUG_DEFAULTS: dict = {}
 

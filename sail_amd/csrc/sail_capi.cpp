@@ -16,6 +16,9 @@
 
 // launch wrappers defined next to the kernels (sail_trace.hip)
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
+// sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
+int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, hipFunction_t* plain,
+                     hipFunction_t* grouped, std::string* err);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
@@ -142,6 +145,10 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
+  int jit = 1;           // SAIL_DEBUG_JIT: scenes on the all-plugin flat kernel get one compiled for their plugin set
+  bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
+  std::string jitError;
+  bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
@@ -216,6 +223,10 @@ int loadIncomplete(sail_ctx* c, const char* what) {
   } while (0)
 
 // the smallest precompiled plugin-set kernel that covers the scene (sail_device.h SAIL_KSET_*)
+// The run-time compiled kernel of the scene's plugin set (sail_jit.cpp) for scenes the precompiled Cornell and room
+// kernels do not cover on the flat path; false when it does not apply or could not be built (the all-plugin kernel
+// then runs, with the same results).
+bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped);
 int kernelSetFor(const sail_ctx* c) {
   if (c->forceGeneric || c->n >= c->cullMinPrims) return SAIL_KSET_GENERIC;
   const sail_plugins& p = c->plugins;
@@ -229,6 +240,19 @@ int kernelSetFor(const sail_ctx* c) {
 
 // the sample-group stage's cap (12 B per owned pixel per staged sample): 8 GiB
 constexpr size_t kStageCapBytes = (size_t)8 << 30;
+bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped) {
+  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric || c->n >= c->cullMinPrims ||
+      kernelSetFor(c) != SAIL_KSET_GENERIC)
+    return false;
+  const sail_plugins& p = c->plugins;
+  std::string err;
+  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, 0, plain, grouped, &err)) {
+    c->jitFailed = true;
+    c->jitError = err;
+    return false;
+  }
+  return true;
+}
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
   const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
   *tilesX = tx; *tilesY = ty;
@@ -692,7 +716,16 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (wavefront) {
       HIPCHK(c, sail_launch_wavefront(A, WS, c->stream));
     } else {
-      HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
+      hipFunction_t jp = nullptr, jg = nullptr;
+      if (A.kernelSet == SAIL_KSET_GENERIC && !A.cullPrims && jitKernels(c, &jp, &jg)) {
+        void* args[] = {&A};
+        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jg : jp, (unsigned)(owned * 16 * A.sampleGroups), 1, 1, 256, 1,
+                                        1, 0, c->stream, args, nullptr));
+        c->lastJit = true;
+      } else {
+        HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
+        c->lastJit = false;
+      }
       if (staged) HIPCHK(c, sail_launch_accum(A, owned * 16, c->stream));
     }
     HIPCHK(c, hipEventRecord(e1, c->stream));
@@ -862,6 +895,7 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
   // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
   if (c->lastWavefront) k = "sail_wf_*";
+  else if (c->lastJit) k = "sail_trace_kernel_jit";
   snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }
@@ -1021,6 +1055,7 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_CULL_FMA: c->cullFma = value; break;
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
+    case SAIL_DEBUG_JIT: c->jit = value; break;
     case SAIL_DEBUG_GROUP_ROUNDS:
       if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
       c->flatGroupRounds = value;
@@ -1070,6 +1105,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   c->plugins = *plugins;
   c->lastGroups = 1;
   c->lastWavefront = false;
+  c->lastJit = false;
   std::vector<SailPrim> prims;
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
@@ -1101,6 +1137,10 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   c->tpRows.assign(texparams, texparams + (size_t)tn * 16);
   c->n = n; c->tn = tn; c->ln = ln;
   c->haveScene = true;
+  {  // Tracer.update links the scene's program (tracer.js:42-90): compile the plugin set's kernel now, not at render
+    hipFunction_t jp, jg;
+    (void)jitKernels(c, &jp, &jg);
+  }
   return resetAccum(c);
 }
 

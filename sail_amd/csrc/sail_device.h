@@ -1,7 +1,15 @@
 // sail_device.h — device-side data layout shared by the trace/filter kernels and the host library.
 // All structs are POD, 16-byte aligned, and identical on host and device.
 #pragma once
+#if defined(__HIPCC_RTC__)  // hipRTC (sail_jit.cpp) has the fixed-width types in its runtime header's namespace
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#else
 #include <stdint.h>
+#endif
 
 // Shape / material / texture / light category ids (src/shader/const/define.glsl:18-44)
 enum {

@@ -1,0 +1,102 @@
+// sail_jit.cpp — per-plugin-set trace kernels compiled at run time with hipRTC.
+//
+// The reference compiles one GLSL program per scene: Scene.tracerConfig() lists the plugins the scene uses
+// (src/scene/scene.js:70-112), Generator.generate assembles exactly those functions (src/shader/generator.js:107-123)
+// and Shader.combinefs links the result (src/core/shader.js:58-76). This build precompiles kernels for two plugin sets
+// (the Cornell box, rooms of boxes / spheres / rectangles) and the all-plugin one; every other scene of the flat path
+// (fewer than 8 primitives) gets a kernel compiled for exactly its plugin set here, from the same sail_trace.hip
+// (embedded in the library at build time, sail_jit_src.cpp), with the product's floating-point flags. Measured before
+// adopting it (profiles/r04_kset_specialised_*.jsonl): the ALL scene +12.0 %, AREA +7.5 % over the all-plugin kernel,
+// bit-identical. Code objects are cached per process and plugin set, modules per device.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+extern const char* const sail_jit_src_names[];
+extern const char* const sail_jit_src_texts[];
+extern const int sail_jit_src_count;
+
+namespace {
+
+struct Key {
+  uint32_t ks, km, kt, kl;
+  int cull;
+  bool operator<(const Key& o) const {
+    return std::tie(ks, km, kt, kl, cull) < std::tie(o.ks, o.km, o.kt, o.kl, o.cull);
+  }
+};
+std::mutex g_jitMutex;
+std::map<std::pair<std::string, Key>, std::vector<char>> g_code;  // (arch, plugin set) -> code object
+struct Loaded { hipModule_t mod; hipFunction_t plain, grouped; };
+std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, plugin set) -> module
+
+// the same floating-point contract as sail_amd/build.sh: no contraction, no fast math, no SLP packing
+int compile(const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
+  char defs[512];
+  snprintf(defs, sizeof defs,
+           "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %s\n#define SAIL_JIT_KS 0x%xu\n"
+           "#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n#define SAIL_JIT_NT %d\n"
+           "#include \"sail_trace.hip\"\n",
+           k.cull ? 8 : 6, k.cull ? "true" : "false", k.ks, k.km, k.kt, k.kl, k.cull ? 1024 : 256);
+  hiprtcProgram prog;
+  hiprtcResult r = hiprtcCreateProgram(&prog, defs, "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts,
+                                       sail_jit_src_names);
+  if (r != HIPRTC_SUCCESS) { err = hiprtcGetErrorString(r); return -1; }
+  const std::string archOpt = "--offload-arch=" + arch;
+  const char* opts[] = {archOpt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                        "-mllvm", "-vectorize-slp=false"};
+  r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  if (r != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    err = std::string(hiprtcGetErrorString(r)) + ": " + log.substr(0, 2000);
+    hiprtcDestroyProgram(&prog);
+    return -1;
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  code.resize(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  return n ? 0 : -1;
+}
+
+}  // namespace
+
+// The trace kernel pair (ungrouped, _grouped) for exactly this plugin set on `device` (the current device), compiled
+// on first use. Returns 0 and the functions, or -1 with a message (the caller then runs the precompiled kernel).
+int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, hipFunction_t* plain,
+                     hipFunction_t* grouped, std::string* err) {
+  const Key k{ks, km, kt, kl, cull ? 1 : 0};
+  std::lock_guard<std::mutex> lock(g_jitMutex);
+  auto it = g_loaded.find({device, k});
+  if (it == g_loaded.end()) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { *err = "hipGetDeviceProperties"; return -1; }
+    std::string arch = prop.gcnArchName;
+    const size_t colon = arch.find(':');  // "gfx950:sramecc+:xnack-": the features follow the device
+    if (colon != std::string::npos) arch = arch.substr(0, colon);
+    auto& code = g_code[{arch, k}];
+    if (code.empty() && compile(arch, k, code, *err)) { g_code.erase({arch, k}); return -1; }
+    Loaded L{};
+    if (hipModuleLoadData(&L.mod, code.data()) != hipSuccess) { *err = "hipModuleLoadData"; return -1; }
+    if (hipModuleGetFunction(&L.plain, L.mod, "sail_trace_kernel_jit") != hipSuccess ||
+        hipModuleGetFunction(&L.grouped, L.mod, "sail_trace_kernel_jit_grouped") != hipSuccess) {
+      (void)hipModuleUnload(L.mod);
+      *err = "hipModuleGetFunction";
+      return -1;
+    }
+    it = g_loaded.emplace(std::make_pair(device, k), L).first;
+  }
+  *plain = it->second.plain;
+  *grouped = it->second.grouped;
+  return 0;
+}

@@ -7,7 +7,9 @@
 // (bounds in DESIGN.md §4). The library is compiled with -ffp-contract=off, so no other FMA is formed. The CPU oracle
 // carries an independent copy of the spec (oracle/ref_math.h); the GPU tests check them bit-for-bit.
 #pragma once
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
+#endif
 
 namespace sm {
 

@@ -3,7 +3,9 @@
 // row 1 and lane 47 to row 3; row_bcast 31 adds lane 31 to rows 2 and 3). Six VALU, no LDS round trips
 // (tools/dpp_scan_probe.hip checks it against a serial scan on the GPU).
 #pragma once
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
+#endif
 __device__ __forceinline__ int waveScanIncl(int x) {
   int v = x;
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1

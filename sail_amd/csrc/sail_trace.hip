@@ -20,8 +20,10 @@
 //  * per-sample camera corners and seeds arrive precomputed (SailSample, scalar loads);
 //  * all f32 math follows the reference expression order with contraction off; transcendentals use
 //    the bit-defined spec in sail_math.h.
+#if !defined(__HIPCC_RTC__)  // hipRTC (the per-plugin-set kernels, sail_jit.cpp) provides the HIP runtime and stdint
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 #include "sail_device.h"
 #include "sail_math.h"
 #include "sail_scan.h"
@@ -1951,6 +1953,13 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   extern "C" __global__ void __launch_bounds__(gnt, waves) name##_grouped(SailTraceArgs A) {                     \
     traceTileCompact<cull, true, ks, km, kt, kl, gnt>(A);                                                        \
   }
+#if defined(SAIL_JIT)
+// A per-plugin-set kernel compiled at run time by hipRTC (sail_jit.cpp), like the reference's per-scene program
+// (tracerConfig -> Generator.generate, src/scene/scene.js:70-112, src/shader/generator.js:107-123): the plugin masks,
+// the pre-cull choice and the launch bounds arrive as macros, and only this kernel pair is compiled.
+SAIL_TRACE_KERNELS(sail_trace_kernel_jit, SAIL_JIT_WAVES, SAIL_JIT_CULL, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
+                   SAIL_JIT_NT, SAIL_JIT_NT)
+#else
 // every plugin (any scene of fewer than 8 primitives outside the two sets below)
 #define SAIL_GENERIC_WAVES 6
 SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_GENERIC_WAVES, false, ~0u, ~0u, ~0u, ~0u, 256, 256)
@@ -2442,3 +2451,4 @@ hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, 
   hipLaunchKernelGGL(sail_math_kernel, dim3((count + 255) / 256), dim3(256), 0, 0, fn, x, y, out, count);
   return hipGetLastError();
 }
+#endif  // !SAIL_JIT

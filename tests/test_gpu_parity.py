@@ -638,3 +638,44 @@ def test_phase_timing_build_bit_exact(gpu, fixtures, monkeypatch, name, W, H, sp
     assert bit_equal(got, want).all()
     assert lib.sail_phase_read(buf, 0) == 0
     assert buf[0] > 0 and buf[1] > 0  # sweep and hit-record phases were timed
+
+
+# ---- per-plugin-set kernels compiled at run time (sail_jit.cpp) ------------------------------------------------
+@pytest.mark.parametrize("name,W,H,spp,B", [("ALL", 40, 32, 3, 6), ("AREA", 36, 28, 3, 5), ("BILERP", 33, 17, 2, 5)])
+def test_jit_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
+    """a scene outside the precompiled Cornell / room sets runs a kernel hipRTC compiled for exactly its plugin set
+    (at sail_set_scene, as the reference links its per-scene program in Tracer.update); its frame equals the
+    oracle's and the all-plugin kernel's bit for bit, in one launch and in sample groups"""
+    sc = fixtures["scenes"][name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    out = {}
+    for label, dbg in (("jit", {}), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0})):
+        ctx = capi.Context(W, H, debug=dbg)
+        try:
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            out[label] = (ctx.read_accum(), ctx.kernel_name())
+        finally:
+            ctx.close()
+    assert out["jit"][1] == "sail_trace_kernel_jit", out["jit"][1]
+    assert out["jit_groups"][1] == "sail_trace_kernel_jit_grouped"
+    assert out["generic"][1] == "sail_trace_kernel"
+    for label, (acc, _) in out.items():
+        assert bit_equal(acc, want).all(), label
+
+
+def test_jit_kernel_multi_device_and_update(gpu, fixtures):
+    """the run-time kernel on a multi-device context (one module per device, the code object compiled once)"""
+    sc = fixtures["scenes"]["ALL"]
+    W, H, spp, B = 48, 40, 2, 5
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    ctx = capi.Context(W, H, devices=[0, 0])
+    try:
+        ctx.set_scene_dict(sc)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        assert bit_equal(ctx.read_accum(), want).all()
+        assert ctx.kernel_name().startswith("sail_trace_kernel_jit")
+    finally:
+        ctx.close()

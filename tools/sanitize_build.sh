@@ -13,12 +13,13 @@ CLANG=/opt/rocm/lib/llvm/bin/clang++
 HIPCC=/opt/rocm/bin/hipcc
 SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -shared-libasan -g -O1"
 [ -f sail_amd/build/sail_trace.o ] || sh sail_amd/build.sh
-for f in sail_capi sail_hostmath; do
+for f in sail_capi sail_hostmath sail_jit; do
   $HIPCC -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $SAN -fno-gpu-sanitize --offload-arch=gfx950 \
     -c sail_amd/csrc/$f.cpp -o $OUT/$f.o
 done
 $HIPCC -shared -fPIC -shared-libasan -fsanitize=address,undefined -fno-gpu-sanitize --offload-arch=gfx950 \
-  sail_amd/build/sail_trace.o $OUT/sail_capi.o $OUT/sail_hostmath.o -o $OUT/libsail_hip_asan.so -ldl
+  sail_amd/build/sail_trace.o $OUT/sail_capi.o $OUT/sail_hostmath.o $OUT/sail_jit.o sail_amd/build/sail_jit_src.o \
+  -o $OUT/libsail_hip_asan.so -ldl -lhiprtc
 $CLANG -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math $SAN oracle/sail_oracle.cpp \
   -o $OUT/libsail_oracle_asan.so
 if [ -d /usr/include/node ]; then
