@@ -119,7 +119,8 @@ enum sail_debug_option {
   SAIL_DEBUG_CULL_GROUP_ROUNDS = 8,
   /* 1: a scene the precompiled Cornell and room kernels do not cover, on the flat path (fewer than
    * SAIL_DEBUG_CULL_MIN_PRIMS primitives), runs a kernel compiled by hipRTC for exactly its plugin set at sail_set_scene
-   * (the reference's per-scene program, src/scene/scene.js:70-112); 0: the all-plugin kernel. Same results [1] */
+   * (the reference's per-scene program, src/scene/scene.js:70-112); 2: the pre-cull path's scenes too; 0: the
+   * all-plugin kernels. Same results [1] */
   SAIL_DEBUG_JIT = 9
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);

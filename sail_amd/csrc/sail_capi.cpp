@@ -241,12 +241,12 @@ int kernelSetFor(const sail_ctx* c) {
 // the sample-group stage's cap (12 B per owned pixel per staged sample): 8 GiB
 constexpr size_t kStageCapBytes = (size_t)8 << 30;
 bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped) {
-  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric || c->n >= c->cullMinPrims ||
-      kernelSetFor(c) != SAIL_KSET_GENERIC)
-    return false;
+  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric || kernelSetFor(c) != SAIL_KSET_GENERIC) return false;
+  const int cull = c->n >= c->cullMinPrims ? 1 : 0;
+  if (cull && c->jit < 2) return false;  // the pre-cull path compiles its plugin set only with SAIL_DEBUG_JIT = 2
   const sail_plugins& p = c->plugins;
   std::string err;
-  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, 0, plain, grouped, &err)) {
+  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, cull, plain, grouped, &err)) {
     c->jitFailed = true;
     c->jitError = err;
     return false;
@@ -717,10 +717,11 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       HIPCHK(c, sail_launch_wavefront(A, WS, c->stream));
     } else {
       hipFunction_t jp = nullptr, jg = nullptr;
-      if (A.kernelSet == SAIL_KSET_GENERIC && !A.cullPrims && jitKernels(c, &jp, &jg)) {
+      if (A.kernelSet == SAIL_KSET_GENERIC && jitKernels(c, &jp, &jg)) {
         void* args[] = {&A};
-        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jg : jp, (unsigned)(owned * 16 * A.sampleGroups), 1, 1, 256, 1,
-                                        1, 0, c->stream, args, nullptr));
+        const unsigned nt = A.cullPrims ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips (sail_launch_trace)
+        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jg : jp, (unsigned)(owned * 16 * A.sampleGroups) * 256u / nt, 1,
+                                        1, nt, 1, 1, 0, c->stream, args, nullptr));
         c->lastJit = true;
       } else {
         HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
@@ -895,7 +896,7 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
   // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
   if (c->lastWavefront) k = "sail_wf_*";
-  else if (c->lastJit) k = "sail_trace_kernel_jit";
+  else if (c->lastJit) k = c->n >= c->cullMinPrims ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
   snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }

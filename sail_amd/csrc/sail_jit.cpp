@@ -40,10 +40,10 @@ std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, plu
 int compile(const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
   char defs[512];
   snprintf(defs, sizeof defs,
-           "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %s\n#define SAIL_JIT_KS 0x%xu\n"
+           "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %d\n#define SAIL_JIT_KS 0x%xu\n"
            "#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n#define SAIL_JIT_NT %d\n"
            "#include \"sail_trace.hip\"\n",
-           k.cull ? 8 : 6, k.cull ? "true" : "false", k.ks, k.km, k.kt, k.kl, k.cull ? 1024 : 256);
+           k.cull ? 8 : 6, k.cull, k.ks, k.km, k.kt, k.kl, k.cull ? 1024 : 256);
   hiprtcProgram prog;
   hiprtcResult r = hiprtcCreateProgram(&prog, defs, "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts,
                                        sail_jit_src_names);
@@ -79,6 +79,7 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
   std::lock_guard<std::mutex> lock(g_jitMutex);
   auto it = g_loaded.find({device, k});
   if (it == g_loaded.end()) {
+    if (hipSetDevice(device) != hipSuccess) { *err = "hipSetDevice"; return -1; }  // the module loads on this device
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { *err = "hipGetDeviceProperties"; return -1; }
     std::string arch = prop.gcnArchName;
@@ -88,8 +89,9 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
     if (code.empty() && compile(arch, k, code, *err)) { g_code.erase({arch, k}); return -1; }
     Loaded L{};
     if (hipModuleLoadData(&L.mod, code.data()) != hipSuccess) { *err = "hipModuleLoadData"; return -1; }
-    if (hipModuleGetFunction(&L.plain, L.mod, "sail_trace_kernel_jit") != hipSuccess ||
-        hipModuleGetFunction(&L.grouped, L.mod, "sail_trace_kernel_jit_grouped") != hipSuccess) {
+    const char* fn = k.cull ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
+    if (hipModuleGetFunction(&L.plain, L.mod, fn) != hipSuccess ||
+        hipModuleGetFunction(&L.grouped, L.mod, (std::string(fn) + "_grouped").c_str()) != hipSuccess) {
       (void)hipModuleUnload(L.mod);
       *err = "hipModuleGetFunction";
       return -1;

@@ -1957,8 +1957,13 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 // A per-plugin-set kernel compiled at run time by hipRTC (sail_jit.cpp), like the reference's per-scene program
 // (tracerConfig -> Generator.generate, src/scene/scene.js:70-112, src/shader/generator.js:107-123): the plugin masks,
 // the pre-cull choice and the launch bounds arrive as macros, and only this kernel pair is compiled.
-SAIL_TRACE_KERNELS(sail_trace_kernel_jit, SAIL_JIT_WAVES, SAIL_JIT_CULL, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
+#if SAIL_JIT_CULL
+SAIL_TRACE_KERNELS(sail_trace_kernel_cull_jit, SAIL_JIT_WAVES, true, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
                    SAIL_JIT_NT, SAIL_JIT_NT)
+#else
+SAIL_TRACE_KERNELS(sail_trace_kernel_jit, SAIL_JIT_WAVES, false, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
+                   SAIL_JIT_NT, SAIL_JIT_NT)
+#endif
 #else
 // every plugin (any scene of fewer than 8 primitives outside the two sets below)
 #define SAIL_GENERIC_WAVES 6

@@ -39,8 +39,12 @@ def test_abi_version():
     assert capi.load().sail_abi_version() == 3
 
 
-def test_library_targets_gfx950():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", capi.LIB_PATH],
+def test_library_targets_gfx950(tmp_path):
+    # llvm-objdump --offloading extracts the bundles next to its input: give it a copy in a scratch directory
+    import shutil
+    lib = str(tmp_path / "libsail_hip.so")
+    shutil.copy(capi.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
                          capture_output=True, text=True)
     text = out.stdout + out.stderr
     if "gfx950" not in text:

@@ -650,7 +650,8 @@ def test_jit_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
     out = {}
-    for label, dbg in (("jit", {}), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0})):
+    one = {capi.DEBUG_SAMPLE_GROUPS: 1}  # a small frame would otherwise split its samples into groups
+    for label, dbg in (("jit", one), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0, **one})):
         ctx = capi.Context(W, H, debug=dbg)
         try:
             ctx.set_scene_dict(sc)
@@ -679,3 +680,24 @@ def test_jit_kernel_multi_device_and_update(gpu, fixtures):
         assert ctx.kernel_name().startswith("sail_trace_kernel_jit")
     finally:
         ctx.close()
+
+
+def test_jit_precull_kernel_bit_exact(gpu, fixtures):
+    """SAIL_DEBUG_JIT = 2: the pre-cull path (C4, 67 rows) compiled for exactly its plugin set, 1,024-thread
+    workgroups like the precompiled pre-cull kernel; bit-exact against the oracle, with and without sample groups"""
+    sc = fixtures["scenes"]["C4"]
+    W, H, spp, B = 40, 24, 2, 6
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    for dbg, name in (({capi.DEBUG_JIT: 2, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_cull_jit"),
+                      ({capi.DEBUG_JIT: 2, capi.DEBUG_SAMPLE_GROUPS: 2}, "sail_trace_kernel_cull_jit_grouped"),
+                      ({capi.DEBUG_JIT: 1, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_cull")):
+        ctx = capi.Context(W, H, debug=dbg)
+        try:
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            got = ctx.read_accum()
+            assert ctx.kernel_name() == name, (dbg, ctx.kernel_name())
+        finally:
+            ctx.close()
+        assert bit_equal(got, want).all(), dbg
