@@ -174,6 +174,14 @@ int sail_save_accum(sail_ctx* ctx, int part, float* sums, uint64_t* k);
  * with a different k fails with SAIL_E_INVALID. The caller checks the sums' size: W*H*4 floats. */
 int sail_load_accum(sail_ctx* ctx, int part, const float* sums, uint64_t k);
 
+/* ---- run-time compiled plugin-set kernels (Scene.tracerConfig -> Generator.generate, src/scene/scene.js:70-112,
+ * src/shader/generator.js:107-123: the reference builds one program per scene plugin set) ----
+ * Host only, no device needed: compile (hipRTC, gfx950) the trace kernel pair for exactly this plugin set, flat
+ * (cull = 0) or pre-cull (cull = 1), from the kernel sources embedded in the library, with the product's floating-point
+ * flags. *bytes = the code object's size; with code != NULL and *bytes large enough on entry it is copied there. The
+ * contexts do the same at sail_set_scene (SAIL_DEBUG_JIT) and load the result on their device. */
+int sail_jit_compile(const sail_plugins* plugins, int cull, void* code, size_t* bytes);
+
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */
 /* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):
  * P*MV (scene.mat, src/scene/scene.js:40-42) as 16 doubles, row-major */

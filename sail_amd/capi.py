@@ -39,7 +39,7 @@ EXPORTS = (
     "sail_filter", "sail_get_stats", "sail_camera", "sail_jitter_inverse", "sail_schedule",
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
     "sail_prim_bounds", "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
-    "sail_abi_version", "sail_accum_parts", "sail_save_accum", "sail_load_accum",
+    "sail_abi_version", "sail_accum_parts", "sail_save_accum", "sail_load_accum", "sail_jit_compile",
 )
 
 
@@ -131,6 +131,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_accum_parts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
         "sail_save_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.POINTER(ctypes.c_uint64)]),
         "sail_load_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.c_uint64]),
+        "sail_jit_compile": (ctypes.c_int, [ctypes.POINTER(Plugins), ctypes.c_int, vp, ctypes.POINTER(ctypes.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -19,6 +19,8 @@ hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 // sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
 int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, hipFunction_t* plain,
                      hipFunction_t* grouped, std::string* err);
+int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, void* code,
+                  size_t* bytes, std::string* err);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
@@ -1599,6 +1601,15 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
     c->samplesThisRank = k > (uint64_t)c->rank ? (k - 1 - (uint64_t)c->rank) / (uint64_t)c->world + 1 : 0;
   else
     c->samplesThisRank = k;
+  return SAIL_OK;
+}
+
+int sail_jit_compile(const sail_plugins* plugins, int cull, void* code, size_t* bytes) {
+  if (!plugins || !bytes) return SAIL_E_INVALID;
+  std::string err;
+  if (sail_jit_code("gfx950", plugins->shape_mask, plugins->material_mask, plugins->texture_mask, plugins->light_mask,
+                    cull, code, bytes, &err))
+    return fail(nullptr, SAIL_E_INVALID, "sail_jit_compile: %s", err.c_str());
   return SAIL_OK;
 }
 

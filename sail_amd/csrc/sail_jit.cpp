@@ -12,6 +12,7 @@
 #include <hip/hiprtc.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -100,5 +101,23 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
   }
   *plain = it->second.plain;
   *grouped = it->second.grouped;
+  return 0;
+}
+
+// Host-only: the code object of the plugin set's kernel pair for `arch`, compiled (not loaded) by the same path
+// (include/sail_hip.h sail_jit_compile). *bytes = its size; copied into `code` when `code` is not null and the
+// buffer (*bytes on entry) is large enough.
+int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, void* code,
+                  size_t* bytes, std::string* err) {
+  const Key k{ks, km, kt, kl, cull ? 1 : 0};
+  std::lock_guard<std::mutex> lock(g_jitMutex);
+  auto& c = g_code[{arch, k}];
+  if (c.empty() && compile(arch, k, c, *err)) { g_code.erase({arch, k}); return -1; }
+  const size_t have = *bytes;
+  *bytes = c.size();
+  if (code) {
+    if (have < c.size()) { *err = "buffer too small"; return -1; }
+    std::copy(c.begin(), c.end(), static_cast<char*>(code));
+  }
   return 0;
 }

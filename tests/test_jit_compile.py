@@ -1,0 +1,74 @@
+"""CPU: the run-time compiled plugin-set kernels (sail_jit.cpp) through the host-only sail_jit_compile. hipRTC compiles
+the kernel sources embedded in the library with the product's floating-point flags: for the all-plugin set the flat
+kernel pair is instruction-for-instruction the precompiled all-plugin kernel pair (so the run-time path cannot differ
+in contraction, fast-math or packing), and specialised sets compile to the kernel names the contexts load."""
+import ctypes
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from sail_amd import capi
+
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def _compile(masks, cull):
+    lib = capi.load()
+    pl = capi.Plugins(*masks)
+    n = ctypes.c_size_t(0)
+    assert lib.sail_jit_compile(ctypes.byref(pl), cull, None, ctypes.byref(n)) == 0, lib.sail_last_error(None)
+    buf = ctypes.create_string_buffer(n.value)
+    assert lib.sail_jit_compile(ctypes.byref(pl), cull, buf, ctypes.byref(n)) == 0
+    small = ctypes.c_size_t(16)
+    assert lib.sail_jit_compile(ctypes.byref(pl), cull, buf, ctypes.byref(small)) != 0  # too small a buffer
+    return buf.raw
+
+
+def _kernels(asm):
+    out, cur = {}, None
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            cur = out.setdefault(m.group(1), [])
+            continue
+        t = re.sub(r"<[^>]*>|\s*//.*", "", re.sub(r"^\s*[0-9a-f]+:\s*", "", line.strip()))
+        if cur is not None and t and not t.startswith(("s_nop", "s_code_end")):  # padding after the last function
+            cur.append(t)
+    return out
+
+
+def _disasm(path):
+    return subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", path], capture_output=True, text=True, check=True).stdout
+
+
+@pytest.fixture(scope="module")
+def product_kernels(tmp_path_factory):
+    d = tmp_path_factory.mktemp("prod")
+    lib = d / "libsail_hip.so"
+    shutil.copy(capi.LIB_PATH, lib)
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], capture_output=True, text=True, cwd=d)
+    co = [p for p in d.iterdir() if "amdgcn" in p.name]
+    assert co, "no gfx950 code object in the library"
+    return _kernels(_disasm(str(co[0])))
+
+
+def test_all_plugin_jit_equals_precompiled_generic(tmp_path, product_kernels):
+    code = _compile([0xFFFFFFFF] * 4, 0)
+    p = tmp_path / "jit.co"
+    p.write_bytes(code)
+    jit = _kernels(_disasm(str(p)))
+    assert set(jit) == {"sail_trace_kernel_jit", "sail_trace_kernel_jit_grouped"}
+    assert jit["sail_trace_kernel_jit"] == product_kernels["sail_trace_kernel"]
+    assert jit["sail_trace_kernel_jit_grouped"] == product_kernels["sail_trace_kernel_grouped"]
+
+
+@pytest.mark.parametrize("scene,cull,name", [("ALL", 0, "sail_trace_kernel_jit"), ("C4", 1, "sail_trace_kernel_cull_jit")])
+def test_plugin_set_kernel_compiles(tmp_path, fixtures, scene, cull, name):
+    code = _compile(capi.plugin_masks(fixtures["scenes"][scene]["plugins"]), cull)
+    p = tmp_path / "jit.co"
+    p.write_bytes(code)
+    asm = _disasm(str(p))
+    assert set(_kernels(asm)) == {name, name + "_grouped"}
+    assert "v_pk_" not in asm  # no SLP packing, as the product build (-fno-slp-vectorize)
