@@ -117,10 +117,11 @@ enum sail_debug_option {
    * pre-cull kernel [64] (SAIL_DEBUG_SAMPLE_GROUPS overrides both) */
   SAIL_DEBUG_GROUP_ROUNDS = 7,
   SAIL_DEBUG_CULL_GROUP_ROUNDS = 8,
-  /* 1: a scene the precompiled Cornell and room kernels do not cover, on the flat path (fewer than
-   * SAIL_DEBUG_CULL_MIN_PRIMS primitives), runs a kernel compiled by hipRTC for exactly its plugin set at sail_set_scene
-   * (the reference's per-scene program, src/scene/scene.js:70-112); 2: the pre-cull path's scenes too; 0: the
-   * all-plugin kernels. Same results [1] */
+  /* which scenes run a kernel compiled by hipRTC for exactly their plugin set at sail_set_scene (the reference's
+   * per-scene program, src/scene/scene.js:70-112), a sum of bits: 1 flat-path scenes (fewer than
+   * SAIL_DEBUG_CULL_MIN_PRIMS primitives) that the precompiled Cornell and room kernels do not cover, 8 those as a
+   * room-family kernel (SAIL_JIT_MODE_ROOM) instead of a plain one, 4 scenes of the room kernel's set, 2 pre-cull-path
+   * scenes. 0: the precompiled kernels only. Same results [1] */
   SAIL_DEBUG_JIT = 9
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
@@ -176,11 +177,16 @@ int sail_load_accum(sail_ctx* ctx, int part, const float* sums, uint64_t k);
 
 /* ---- run-time compiled plugin-set kernels (Scene.tracerConfig -> Generator.generate, src/scene/scene.js:70-112,
  * src/shader/generator.js:107-123: the reference builds one program per scene plugin set) ----
- * Host only, no device needed: compile (hipRTC, gfx950) the trace kernel pair for exactly this plugin set, flat
- * (cull = 0) or pre-cull (cull = 1), from the kernel sources embedded in the library, with the product's floating-point
- * flags. *bytes = the code object's size; with code != NULL and *bytes large enough on entry it is copied there. The
+ * Host only, no device needed: compile (hipRTC, gfx950) the trace kernel pair for exactly this plugin set in one of the
+ * kernel forms below, from the kernel sources embedded in the library, with the product's floating-point flags.
+ * *bytes = the code object's size; with code != NULL and *bytes large enough on entry it is copied there. The
  * contexts do the same at sail_set_scene (SAIL_DEBUG_JIT) and load the result on their device. */
-int sail_jit_compile(const sail_plugins* plugins, int cull, void* code, size_t* bytes);
+enum sail_jit_mode {
+  SAIL_JIT_MODE_FLAT = 0, /* flat path, the all-plugin kernel's form (6 waves per SIMD, three-barrier sort) */
+  SAIL_JIT_MODE_CULL = 1, /* pre-cull path (1,024-thread workgroups) */
+  SAIL_JIT_MODE_ROOM = 2  /* flat path, the room kernel's form (7 waves, two-barrier sort, first sample group at home) */
+};
+int sail_jit_compile(const sail_plugins* plugins, int mode, void* code, size_t* bytes);
 
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */
 /* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):

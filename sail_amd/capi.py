@@ -28,6 +28,7 @@ DEBUG_WAVEFRONT = 6
 DEBUG_GROUP_ROUNDS = 7
 DEBUG_CULL_GROUP_ROUNDS = 8
 DEBUG_JIT = 9
+JIT_MODE_FLAT, JIT_MODE_CULL, JIT_MODE_ROOM = 0, 1, 2  # sail_jit_compile kernel forms (include/sail_hip.h)
 # applied to every Context at creation (tests set entries with monkeypatch.setitem)
 DEBUG_DEFAULTS: dict = {}
 

@@ -17,9 +17,9 @@
 // launch wrappers defined next to the kernels (sail_trace.hip)
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 // sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
-int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, hipFunction_t* plain,
+int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, hipFunction_t* plain,
                      hipFunction_t* grouped, std::string* err);
-int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, void* code,
+int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, void* code,
                   size_t* bytes, std::string* err);
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
@@ -147,10 +147,11 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int jit = 1;           // SAIL_DEBUG_JIT: scenes on the all-plugin flat kernel get one compiled for their plugin set
+  int jit = 1;           // SAIL_DEBUG_JIT bits: which scenes get a kernel compiled for their plugin set (jitKernels)
   bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
   std::string jitError;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
+  int lastJitMode = 0;
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
@@ -225,10 +226,9 @@ int loadIncomplete(sail_ctx* c, const char* what) {
   } while (0)
 
 // the smallest precompiled plugin-set kernel that covers the scene (sail_device.h SAIL_KSET_*)
-// The run-time compiled kernel of the scene's plugin set (sail_jit.cpp) for scenes the precompiled Cornell and room
-// kernels do not cover on the flat path; false when it does not apply or could not be built (the all-plugin kernel
-// then runs, with the same results).
-bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped);
+// The run-time compiled kernel of the scene's plugin set (sail_jit.cpp); false when it does not apply or could not be
+// built (the precompiled kernel of the scene's set then runs, with the same results). *mode: SAIL_JIT_MODE_*.
+bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* mode);
 int kernelSetFor(const sail_ctx* c) {
   if (c->forceGeneric || c->n >= c->cullMinPrims) return SAIL_KSET_GENERIC;
   const sail_plugins& p = c->plugins;
@@ -242,17 +242,32 @@ int kernelSetFor(const sail_ctx* c) {
 
 // the sample-group stage's cap (12 B per owned pixel per staged sample): 8 GiB
 constexpr size_t kStageCapBytes = (size_t)8 << 30;
-bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped) {
-  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric || kernelSetFor(c) != SAIL_KSET_GENERIC) return false;
-  const int cull = c->n >= c->cullMinPrims ? 1 : 0;
-  if (cull && c->jit < 2) return false;  // the pre-cull path compiles its plugin set only with SAIL_DEBUG_JIT = 2
+// SAIL_DEBUG_JIT bits (include/sail_hip.h): 1 flat scenes outside the Cornell and room sets, 2 pre-cull scenes, 4 room-set
+// scenes (room family), 8 the flat scenes of bit 1 as room family.
+bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* mode) {
+  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric) return false;
+  const int set = kernelSetFor(c);
+  int m;
+  if (set == SAIL_KSET_GENERIC && c->n >= c->cullMinPrims) {
+    if (!(c->jit & 2)) return false;
+    m = SAIL_JIT_MODE_CULL;
+  } else if (set == SAIL_KSET_GENERIC) {
+    if (!(c->jit & 1)) return false;
+    m = (c->jit & 8) ? SAIL_JIT_MODE_ROOM : SAIL_JIT_MODE_FLAT;
+  } else if (set == SAIL_KSET_ROOM) {
+    if (!(c->jit & 4)) return false;
+    m = SAIL_JIT_MODE_ROOM;
+  } else {
+    return false;  // the Cornell kernel's set is the Cornell box's own
+  }
   const sail_plugins& p = c->plugins;
   std::string err;
-  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, cull, plain, grouped, &err)) {
+  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, m, plain, grouped, &err)) {
     c->jitFailed = true;
     c->jitError = err;
     return false;
   }
+  *mode = m;
   return true;
 }
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
@@ -683,7 +698,11 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (nspp > stageSpp) G = 1;  // the stage would pass its cap
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
-    A.groupHome = SAIL_GROUP_HOME_FOR(A.kernelSet) ? 1 : 0;
+    const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
+    hipFunction_t jp = nullptr, jg = nullptr;
+    int jmode = 0;
+    const bool jit = !wavefront && jitKernels(c, &jp, &jg, &jmode);
+    A.groupHome = (jit ? jmode == SAIL_JIT_MODE_ROOM : SAIL_GROUP_HOME_FOR(A.kernelSet)) ? 1 : 0;
     A.stageStride = stageStride;
     const bool staged = A.sampleGroups > 1;
     if (staged) {  // sized for this launch's samples (it grows to the largest launch seen)
@@ -696,7 +715,6 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       }
       A.stage = c->stage;
     }
-    const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
     SailWfState WS;
     memset(&WS, 0, sizeof WS);
     if (wavefront) {
@@ -718,13 +736,13 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (wavefront) {
       HIPCHK(c, sail_launch_wavefront(A, WS, c->stream));
     } else {
-      hipFunction_t jp = nullptr, jg = nullptr;
-      if (A.kernelSet == SAIL_KSET_GENERIC && jitKernels(c, &jp, &jg)) {
+      if (jit) {
         void* args[] = {&A};
-        const unsigned nt = A.cullPrims ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips (sail_launch_trace)
+        const unsigned nt = jmode == SAIL_JIT_MODE_CULL ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips
         HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jg : jp, (unsigned)(owned * 16 * A.sampleGroups) * 256u / nt, 1,
                                         1, nt, 1, 1, 0, c->stream, args, nullptr));
         c->lastJit = true;
+        c->lastJitMode = jmode;
       } else {
         HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
         c->lastJit = false;
@@ -898,7 +916,7 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
                   : (c->n >= c->cullMinPrims ? "sail_trace_kernel_cull" : "sail_trace_kernel");
   // the last launch's form: sample groups run the _grouped kernel followed by sail_accum_kernel
   if (c->lastWavefront) k = "sail_wf_*";
-  else if (c->lastJit) k = c->n >= c->cullMinPrims ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
+  else if (c->lastJit) k = c->lastJitMode == SAIL_JIT_MODE_CULL ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
   snprintf(name, (size_t)len, "%s%s", k, (!c->lastWavefront && c->lastGroups > 1) ? "_grouped" : "");
   return SAIL_OK;
 }
@@ -1142,7 +1160,8 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   c->haveScene = true;
   {  // Tracer.update links the scene's program (tracer.js:42-90): compile the plugin set's kernel now, not at render
     hipFunction_t jp, jg;
-    (void)jitKernels(c, &jp, &jg);
+    int jm;
+    (void)jitKernels(c, &jp, &jg, &jm);
   }
   return resetAccum(c);
 }
@@ -1604,11 +1623,11 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
   return SAIL_OK;
 }
 
-int sail_jit_compile(const sail_plugins* plugins, int cull, void* code, size_t* bytes) {
-  if (!plugins || !bytes) return SAIL_E_INVALID;
+int sail_jit_compile(const sail_plugins* plugins, int mode, void* code, size_t* bytes) {
+  if (!plugins || !bytes || mode < SAIL_JIT_MODE_FLAT || mode > SAIL_JIT_MODE_ROOM) return SAIL_E_INVALID;
   std::string err;
   if (sail_jit_code("gfx950", plugins->shape_mask, plugins->material_mask, plugins->texture_mask, plugins->light_mask,
-                    cull, code, bytes, &err))
+                    mode, code, bytes, &err))
     return fail(nullptr, SAIL_E_INVALID, "sail_jit_compile: %s", err.c_str());
   return SAIL_OK;
 }

@@ -4,7 +4,7 @@
 // (src/scene/scene.js:70-112), Generator.generate assembles exactly those functions (src/shader/generator.js:107-123)
 // and Shader.combinefs links the result (src/core/shader.js:58-76). This build precompiles kernels for two plugin sets
 // (the Cornell box, rooms of boxes / spheres / rectangles) and the all-plugin one; every other scene of the flat path
-// (fewer than 8 primitives) gets a kernel compiled for exactly its plugin set here, from the same sail_trace.hip
+// (fewer than 8 primitives) can get a kernel compiled for exactly its plugin set here, from the same sail_trace.hip
 // (embedded in the library at build time, sail_jit_src.cpp), with the product's floating-point flags. Measured before
 // adopting it (profiles/r04_kset_specialised_*.jsonl): the ALL scene +12.0 %, AREA +7.5 % over the all-plugin kernel,
 // bit-identical. Code objects are cached per process and plugin set, modules per device.
@@ -25,13 +25,16 @@ extern const int sail_jit_src_count;
 
 namespace {
 
+// mode: 0 flat (the all-plugin kernel's form), 1 pre-cull, 2 flat in the room kernel's form (sail_hip.h sail_jit_mode)
 struct Key {
   uint32_t ks, km, kt, kl;
-  int cull;
+  int mode;
   bool operator<(const Key& o) const {
-    return std::tie(ks, km, kt, kl, cull) < std::tie(o.ks, o.km, o.kt, o.kl, o.cull);
+    return std::tie(ks, km, kt, kl, mode) < std::tie(o.ks, o.km, o.kt, o.kl, o.mode);
   }
 };
+// launch bounds of each form: the precompiled kernels' (sail_trace.hip SAIL_*_WAVES / _NT)
+constexpr int kWaves[3] = {6, 8, 7}, kThreads[3] = {256, 1024, 256};
 std::mutex g_jitMutex;
 std::map<std::pair<std::string, Key>, std::vector<char>> g_code;  // (arch, plugin set) -> code object
 struct Loaded { hipModule_t mod; hipFunction_t plain, grouped; };
@@ -41,10 +44,10 @@ std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, plu
 int compile(const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
   char defs[512];
   snprintf(defs, sizeof defs,
-           "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %d\n#define SAIL_JIT_KS 0x%xu\n"
-           "#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n#define SAIL_JIT_NT %d\n"
-           "#include \"sail_trace.hip\"\n",
-           k.cull ? 8 : 6, k.cull, k.ks, k.km, k.kt, k.kl, k.cull ? 1024 : 256);
+           "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %d\n#define SAIL_JIT_FAM %d\n"
+           "#define SAIL_JIT_KS 0x%xu\n#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n"
+           "#define SAIL_JIT_NT %d\n#include \"sail_trace.hip\"\n",
+           kWaves[k.mode], k.mode == 1, k.mode == 2, k.ks, k.km, k.kt, k.kl, kThreads[k.mode]);
   hiprtcProgram prog;
   hiprtcResult r = hiprtcCreateProgram(&prog, defs, "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts,
                                        sail_jit_src_names);
@@ -74,9 +77,10 @@ int compile(const std::string& arch, const Key& k, std::vector<char>& code, std:
 
 // The trace kernel pair (ungrouped, _grouped) for exactly this plugin set on `device` (the current device), compiled
 // on first use. Returns 0 and the functions, or -1 with a message (the caller then runs the precompiled kernel).
-int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, hipFunction_t* plain,
+int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, hipFunction_t* plain,
                      hipFunction_t* grouped, std::string* err) {
-  const Key k{ks, km, kt, kl, cull ? 1 : 0};
+  if (mode < 0 || mode > 2) { *err = "unknown kernel form"; return -1; }
+  const Key k{ks, km, kt, kl, mode};
   std::lock_guard<std::mutex> lock(g_jitMutex);
   auto it = g_loaded.find({device, k});
   if (it == g_loaded.end()) {
@@ -90,7 +94,7 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
     if (code.empty() && compile(arch, k, code, *err)) { g_code.erase({arch, k}); return -1; }
     Loaded L{};
     if (hipModuleLoadData(&L.mod, code.data()) != hipSuccess) { *err = "hipModuleLoadData"; return -1; }
-    const char* fn = k.cull ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
+    const char* fn = k.mode == 1 ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
     if (hipModuleGetFunction(&L.plain, L.mod, fn) != hipSuccess ||
         hipModuleGetFunction(&L.grouped, L.mod, (std::string(fn) + "_grouped").c_str()) != hipSuccess) {
       (void)hipModuleUnload(L.mod);
@@ -107,9 +111,10 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
 // Host-only: the code object of the plugin set's kernel pair for `arch`, compiled (not loaded) by the same path
 // (include/sail_hip.h sail_jit_compile). *bytes = its size; copied into `code` when `code` is not null and the
 // buffer (*bytes on entry) is large enough.
-int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int cull, void* code,
+int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, void* code,
                   size_t* bytes, std::string* err) {
-  const Key k{ks, km, kt, kl, cull ? 1 : 0};
+  if (mode < 0 || mode > 2) { *err = "unknown kernel form"; return -1; }
+  const Key k{ks, km, kt, kl, mode};
   std::lock_guard<std::mutex> lock(g_jitMutex);
   auto& c = g_code[{arch, k}];
   if (c.empty() && compile(arch, k, c, *err)) { g_code.erase({arch, k}); return -1; }

@@ -1017,7 +1017,8 @@ D V3 rectLocalHit(const SailPrim& p, const Ray& r, float t) {
   const V3 o = worldToLocal(r.o - P3(p, 0), f.normal, f.ss, f.ts);
   return o + t * d;
 }
-template <bool RECOMP_HL = false>
+// BOXU: the room family's one box record for Cube and Cornellbox (boxHit)
+template <bool RECOMP_HL = false, bool BOXU = false>
 D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   const float best = sw.best;
   const int bi = sw.bi;
@@ -1030,7 +1031,7 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
 #define BHL (RECOMP_HL ? quadLocalHit(p, r, best) : sw.bhl)
   // compile-time constants: the room kernel's shared box record (boxHit), the pre-cull kernel's shared local-space
   // record (localHit)
-  const bool boxU = c.kShapes == SAIL_KSET_ROOM_SHAPES;
+  constexpr bool boxU = BOXU;
   const bool localU = c.cullPrims != 0;
   const uint32_t kLocal = c.kShapes & ((1u << SAIL_SPHERE) | (1u << SAIL_CONE) | (1u << SAIL_CYLINDER) |
                                        (1u << SAIL_HYPERBOLOID) | (1u << SAIL_PARABOLOID) | (1u << SAIL_DISK));
@@ -1067,15 +1068,15 @@ D Hit hitRecord(const Ctx& c, const Ray& r, const Sweep& sw) {
   return h;
 }
 // wave-uniform winner: the same record with the row index in an SGPR (scalar row loads)
-template <bool RECOMP_HL = false>
+template <bool RECOMP_HL = false, bool BOXU = false>
 D Hit hitRecordU(const Ctx& c, const Ray& r, const Sweep& sw) {
   const int b0 = __builtin_amdgcn_readfirstlane(sw.bi);
   if (__all(sw.bi == b0)) {
     Sweep su = sw;
     su.bi = b0;
-    return hitRecord<RECOMP_HL>(c, r, su);
+    return hitRecord<RECOMP_HL, BOXU>(c, r, su);
   }
-  return hitRecord<RECOMP_HL>(c, r, sw);
+  return hitRecord<RECOMP_HL, BOXU>(c, r, sw);
 }
 
 // ---- sampleGeometry for area lights (shader.shape.js:53-67) -----------------------------------------------------
@@ -1623,7 +1624,7 @@ D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
 // larger pool of paths (fewer mixed waves) at the price of a wider barrier.
 constexpr int kCullLdsRows = 72, kCullLdsTp = 136;
 constexpr int kPrioMixed = 2;
-template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT = 256>
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
@@ -1648,7 +1649,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr bool kShCompact = CULL && KL != 0u;
   __shared__ int sShCnt[2];
   int shph = 0;
-  constexpr bool twoBar = CULL || KS == SAIL_KSET_ROOM_SHAPES;
+  constexpr bool twoBar = CULL || FAM;
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
   const TileWork tw = tileWork<GROUPED, NT>(A);
@@ -1712,8 +1713,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   const bool byPrim = A.n < kKeys;
   const size_t pixG = (size_t)y * A.W + x;
   constexpr bool grouped = GROUPED;
-  // the room kernel's first group accumulates its samples itself (SAIL_GROUP_HOME_FOR, sail_device.h)
-  constexpr bool kHome = KS == SAIL_KSET_ROOM_SHAPES && !CULL;
+  // a room-family kernel's first group accumulates its samples itself (SailTraceArgs.groupHome)
+  constexpr bool kHome = FAM && !CULL;
   const bool home = !grouped || (kHome && tw.kBeg == 0);
   float4 acc = (valid && home) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
@@ -1852,7 +1853,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         }
         c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
         c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
-        const Hit ins = hitRecordU<true>(c, ray, sw);
+        const Hit ins = hitRecordU<true, FAM && !CULL>(c, ray, sw);
         PHASE_MARK(pc, 1);
         if (depth == 1 && aovSample) {
           const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
@@ -1946,45 +1947,47 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 // Each plugin set has an ungrouped kernel (one workgroup per 16 x NT/16 block, every sample) and a _grouped one
 // (sample groups: G workgroups per block, staged radiance added by sail_accum_kernel). Launch bounds: waves per SIMD
 // and threads per workgroup, chosen by the occupancy sweeps of DESIGN.md §5 (sail_launch_trace sizes the grids).
-#define SAIL_TRACE_KERNELS(name, waves, cull, ks, km, kt, kl, nt, gnt)                                               \
+// fam: the room family's choices for a flat kernel -- the two-barrier sort, the first sample group accumulating its
+// samples itself (SailTraceArgs.groupHome) and one box record for Cube and Cornellbox.
+#define SAIL_TRACE_KERNELS(name, waves, cull, ks, km, kt, kl, nt, gnt, fam)                                          \
   extern "C" __global__ void __launch_bounds__(nt, waves) name(SailTraceArgs A) {                                \
-    traceTileCompact<cull, false, ks, km, kt, kl, nt>(A);                                                        \
+    traceTileCompact<cull, false, ks, km, kt, kl, nt, fam>(A);                                                   \
   }                                                                                                              \
   extern "C" __global__ void __launch_bounds__(gnt, waves) name##_grouped(SailTraceArgs A) {                     \
-    traceTileCompact<cull, true, ks, km, kt, kl, gnt>(A);                                                        \
+    traceTileCompact<cull, true, ks, km, kt, kl, gnt, fam>(A);                                                   \
   }
 #if defined(SAIL_JIT)
 // A per-plugin-set kernel compiled at run time by hipRTC (sail_jit.cpp), like the reference's per-scene program
 // (tracerConfig -> Generator.generate, src/scene/scene.js:70-112, src/shader/generator.js:107-123): the plugin masks,
-// the pre-cull choice and the launch bounds arrive as macros, and only this kernel pair is compiled.
+// the pre-cull choice, the family and the launch bounds arrive as macros, and only this kernel pair is compiled.
 #if SAIL_JIT_CULL
 SAIL_TRACE_KERNELS(sail_trace_kernel_cull_jit, SAIL_JIT_WAVES, true, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
-                   SAIL_JIT_NT, SAIL_JIT_NT)
+                   SAIL_JIT_NT, SAIL_JIT_NT, false)
 #else
 SAIL_TRACE_KERNELS(sail_trace_kernel_jit, SAIL_JIT_WAVES, false, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
-                   SAIL_JIT_NT, SAIL_JIT_NT)
+                   SAIL_JIT_NT, SAIL_JIT_NT, SAIL_JIT_FAM != 0)
 #endif
 #else
 // every plugin (any scene of fewer than 8 primitives outside the two sets below)
 #define SAIL_GENERIC_WAVES 6
-SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_GENERIC_WAVES, false, ~0u, ~0u, ~0u, ~0u, 256, 256)
+SAIL_TRACE_KERNELS(sail_trace_kernel, SAIL_GENERIC_WAVES, false, ~0u, ~0u, ~0u, ~0u, 256, 256, false)
 // the README Cornell box plugin set (C1/C2/C5): Cube + Sphere + Cornellbox, Matte + Mirror, uniform colours
 #define SAIL_CORNELL_WAVES 8
 #define SAIL_CORNELL_NT 256
 #define SAIL_CORNELL_GROUP_NT 256
 SAIL_TRACE_KERNELS(sail_trace_kernel_cornell, SAIL_CORNELL_WAVES, false, SAIL_KSET_CORNELL_SHAPES, SAIL_KSET_CORNELL_MATS,
-                   SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT)
+                   SAIL_KSET_CORNELL_TEX, SAIL_KSET_CORNELL_LIGHTS, SAIL_CORNELL_NT, SAIL_CORNELL_GROUP_NT, false)
 // rooms of boxes, spheres and rectangle lights (C3 materials demo, UI demo); occupancy measured 5/6/7/8 waves
 #define SAIL_ROOM_WAVES 7
 #define SAIL_ROOM_NT 256
 #define SAIL_ROOM_GROUP_NT 256
 SAIL_TRACE_KERNELS(sail_trace_kernel_room, SAIL_ROOM_WAVES, false, SAIL_KSET_ROOM_SHAPES, SAIL_KSET_ROOM_MATS,
-                   SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT)
+                   SAIL_KSET_ROOM_TEX, SAIL_KSET_ROOM_LIGHTS, SAIL_ROOM_NT, SAIL_ROOM_GROUP_NT, true)
 // the pre-cull kernel serves scenes with many primitives (C4); 1,024-thread workgroups (16 x 64 strips)
 #define SAIL_CULL_WAVES 8
 #define SAIL_CULL_NT 1024
 #define SAIL_CULL_GROUP_NT 1024
-SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_CULL_WAVES, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT, SAIL_CULL_GROUP_NT)
+SAIL_TRACE_KERNELS(sail_trace_kernel_cull, SAIL_CULL_WAVES, true, ~0u, ~0u, ~0u, ~0u, SAIL_CULL_NT, SAIL_CULL_GROUP_NT, false)
 
 // ---- wavefront split of the pre-cull path (study switch SAIL_DEBUG_WAVEFRONT; DESIGN.md §9 of round 2) -------------------
 // The megakernel keeps each path in registers and LDS across its bounces and sorts the workgroup's paths between the

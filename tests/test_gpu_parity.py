@@ -651,7 +651,9 @@ def test_jit_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
     out = {}
     one = {capi.DEBUG_SAMPLE_GROUPS: 1}  # a small frame would otherwise split its samples into groups
-    for label, dbg in (("jit", one), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0, **one})):
+    room = {capi.DEBUG_JIT: 1 | 8}  # the same scenes in the room kernel's form (SAIL_JIT_MODE_ROOM)
+    for label, dbg in (("jit", one), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0, **one}),
+                       ("jit_room", {**room, **one}), ("jit_room_groups", {**room, capi.DEBUG_SAMPLE_GROUPS: 3})):
         ctx = capi.Context(W, H, debug=dbg)
         try:
             ctx.set_scene_dict(sc)
@@ -659,8 +661,8 @@ def test_jit_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
             out[label] = (ctx.read_accum(), ctx.kernel_name())
         finally:
             ctx.close()
-    assert out["jit"][1] == "sail_trace_kernel_jit", out["jit"][1]
-    assert out["jit_groups"][1] == "sail_trace_kernel_jit_grouped"
+    assert out["jit"][1] == out["jit_room"][1] == "sail_trace_kernel_jit", out["jit"][1]
+    assert out["jit_groups"][1] == out["jit_room_groups"][1] == "sail_trace_kernel_jit_grouped"
     assert out["generic"][1] == "sail_trace_kernel"
     for label, (acc, _) in out.items():
         assert bit_equal(acc, want).all(), label
@@ -682,15 +684,38 @@ def test_jit_kernel_multi_device_and_update(gpu, fixtures):
         ctx.close()
 
 
+@pytest.mark.parametrize("name,W,H,spp,B", [("C3", 40, 36, 3, 6), ("UI", 36, 28, 3, 5)])
+def test_jit_room_set_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
+    """SAIL_DEBUG_JIT bit 4: a scene of the room kernel's set compiled for exactly its plugin set in the room kernel's
+    form (first sample group accumulating at home, the others staged); bit-exact against the oracle and the
+    precompiled room kernel, in one launch and in 2 and 3 sample groups"""
+    sc = fixtures["scenes"][name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    for dbg, kname in (({capi.DEBUG_JIT: 5, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_jit"),
+                       ({capi.DEBUG_JIT: 5, capi.DEBUG_SAMPLE_GROUPS: 2}, "sail_trace_kernel_jit_grouped"),
+                       ({capi.DEBUG_JIT: 5, capi.DEBUG_SAMPLE_GROUPS: 3}, "sail_trace_kernel_jit_grouped"),
+                       ({capi.DEBUG_JIT: 1, capi.DEBUG_SAMPLE_GROUPS: 2}, "sail_trace_kernel_room_grouped")):
+        ctx = capi.Context(W, H, debug=dbg)
+        try:
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            got = ctx.read_accum()
+            assert ctx.kernel_name() == kname, (dbg, ctx.kernel_name())
+        finally:
+            ctx.close()
+        assert bit_equal(got, want).all(), dbg
+
+
 def test_jit_precull_kernel_bit_exact(gpu, fixtures):
-    """SAIL_DEBUG_JIT = 2: the pre-cull path (C4, 67 rows) compiled for exactly its plugin set, 1,024-thread
+    """SAIL_DEBUG_JIT bit 2: the pre-cull path (C4, 67 rows) compiled for exactly its plugin set, 1,024-thread
     workgroups like the precompiled pre-cull kernel; bit-exact against the oracle, with and without sample groups"""
     sc = fixtures["scenes"]["C4"]
     W, H, spp, B = 40, 24, 2, 6
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
-    for dbg, name in (({capi.DEBUG_JIT: 2, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_cull_jit"),
-                      ({capi.DEBUG_JIT: 2, capi.DEBUG_SAMPLE_GROUPS: 2}, "sail_trace_kernel_cull_jit_grouped"),
+    for dbg, name in (({capi.DEBUG_JIT: 3, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_cull_jit"),
+                      ({capi.DEBUG_JIT: 3, capi.DEBUG_SAMPLE_GROUPS: 2}, "sail_trace_kernel_cull_jit_grouped"),
                       ({capi.DEBUG_JIT: 1, capi.DEBUG_SAMPLE_GROUPS: 1}, "sail_trace_kernel_cull")):
         ctx = capi.Context(W, H, debug=dbg)
         try:

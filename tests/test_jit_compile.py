@@ -64,11 +64,32 @@ def test_all_plugin_jit_equals_precompiled_generic(tmp_path, product_kernels):
     assert jit["sail_trace_kernel_jit_grouped"] == product_kernels["sail_trace_kernel_grouped"]
 
 
-@pytest.mark.parametrize("scene,cull,name", [("ALL", 0, "sail_trace_kernel_jit"), ("C4", 1, "sail_trace_kernel_cull_jit")])
-def test_plugin_set_kernel_compiles(tmp_path, fixtures, scene, cull, name):
-    code = _compile(capi.plugin_masks(fixtures["scenes"][scene]["plugins"]), cull)
+@pytest.mark.parametrize("scene,mode,name", [("ALL", 0, "sail_trace_kernel_jit"), ("C4", 1, "sail_trace_kernel_cull_jit"),
+                                             ("ALL", 2, "sail_trace_kernel_jit"), ("C3", 2, "sail_trace_kernel_jit")])
+def test_plugin_set_kernel_compiles(tmp_path, fixtures, scene, mode, name):
+    """every kernel form (sail_jit_mode: flat, pre-cull, flat in the room kernel's form) compiles for a scene's set"""
+    code = _compile(capi.plugin_masks(fixtures["scenes"][scene]["plugins"]), mode)
     p = tmp_path / "jit.co"
     p.write_bytes(code)
     asm = _disasm(str(p))
     assert set(_kernels(asm)) == {name, name + "_grouped"}
     assert "v_pk_" not in asm  # no SLP packing, as the product build (-fno-slp-vectorize)
+
+
+def test_room_form_of_the_room_set_equals_precompiled_room_kernel(tmp_path, product_kernels):
+    """SAIL_JIT_MODE_ROOM compiled for the room kernel's own plugin set is the same kernel pair as the precompiled
+    sail_trace_kernel_room (same source, launch bounds and flags)"""
+    shapes = sum(1 << t for t in (1, 2, 3, 9))  # SAIL_KSET_ROOM_SHAPES: Cube, Sphere, Rectangle, Cornellbox
+    code = _compile([shapes, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF], 2)
+    p = tmp_path / "jit.co"
+    p.write_bytes(code)
+    jit = _kernels(_disasm(str(p)))
+    assert jit["sail_trace_kernel_jit"] == product_kernels["sail_trace_kernel_room"]
+    assert jit["sail_trace_kernel_jit_grouped"] == product_kernels["sail_trace_kernel_room_grouped"]
+
+
+def test_unknown_mode_refused():
+    lib = capi.load()
+    pl = capi.Plugins(1, 1, 0, 0)
+    n = ctypes.c_size_t(0)
+    assert lib.sail_jit_compile(ctypes.byref(pl), 3, None, ctypes.byref(n)) != 0
