@@ -20,5 +20,5 @@ $HIPCC $COMMON --offload-arch=$ARCH -c build/sail_jit_src.cpp -o build/sail_jit_
 wait
 HOST="build/sail_capi.o build/sail_hostmath.o build/sail_jit.o build/sail_jit_src.o"
 for o in build/sail_trace.o build/sail_trace_phase.o $HOST; do [ -s $o ] || { echo "missing $o"; exit 1; }; done
-$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o $HOST -o lib/libsail_hip.so -ldl -lhiprtc
-$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace_phase.o $HOST -o lib/libsail_hip_phase.so -ldl -lhiprtc
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace.o $HOST -o lib/libsail_hip.so -ldl
+$HIPCC -shared -fPIC --offload-arch=$ARCH build/sail_trace_phase.o $HOST -o lib/libsail_hip_phase.so -ldl

@@ -3,15 +3,22 @@
 // The reference compiles one GLSL program per scene: Scene.tracerConfig() lists the plugins the scene uses
 // (src/scene/scene.js:70-112), Generator.generate assembles exactly those functions (src/shader/generator.js:107-123)
 // and Shader.combinefs links the result (src/core/shader.js:58-76). This build precompiles kernels for two plugin sets
-// (the Cornell box, rooms of boxes / spheres / rectangles) and the all-plugin one; every other scene of the flat path
-// (fewer than 8 primitives) can get a kernel compiled for exactly its plugin set here, from the same sail_trace.hip
-// (embedded in the library at build time, sail_jit_src.cpp), with the product's floating-point flags. Measured before
-// adopting it (profiles/r04_kset_specialised_*.jsonl): the ALL scene +12.0 %, AREA +7.5 % over the all-plugin kernel,
-// bit-identical. Code objects are cached per process and plugin set, modules per device.
+// (the Cornell box, rooms of boxes / spheres / rectangles) and the all-plugin one; other scenes can get a kernel
+// compiled for exactly their plugin set here, from the same sail_trace.hip (embedded in the library at build time,
+// sail_jit_src.cpp), with the product's floating-point flags. Measured (profiles/r04_jit_vs_generic.jsonl): ALL +4.1 %,
+// AREA +6.1 %, BILERP +4.6 % over the all-plugin kernel, bit-identical. Code objects are cached per process and plugin
+// set, modules per device.
+//
+// The compiler is the ROCm toolchain's own hipRTC (and the comgr it loads), opened in a link namespace of its own
+// (dlmopen): a process that loaded another HIP runtime first -- PyTorch ships hipRTC and comgr of an older ROCm under
+// the same sonames -- would otherwise compile with that one, and the kernels would differ from the precompiled ones
+// (tests/test_jit_compile.py checks instruction identity after importing torch).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -40,6 +47,47 @@ std::map<std::pair<std::string, Key>, std::vector<char>> g_code;  // (arch, plug
 struct Loaded { hipModule_t mod; hipFunction_t plain, grouped; };
 std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, plugin set) -> module
 
+// hipRTC entry points from the toolchain's library (SAIL_HIPRTC, else $ROCM_PATH or /opt/rocm, lib/libhiprtc.so.7)
+struct Rtc {
+  decltype(&hiprtcCreateProgram) create;
+  decltype(&hiprtcCompileProgram) compile;
+  decltype(&hiprtcGetProgramLogSize) logSize;
+  decltype(&hiprtcGetProgramLog) log;
+  decltype(&hiprtcGetCodeSize) codeSize;
+  decltype(&hiprtcGetCode) code;
+  decltype(&hiprtcDestroyProgram) destroy;
+  decltype(&hiprtcGetErrorString) errStr;
+};
+const Rtc* rtc(std::string& err) {  // under g_jitMutex
+  static Rtc r;
+  static bool tried = false, ok = false;
+  static std::string why;
+  if (!tried) {
+    tried = true;
+    std::string path;
+    if (const char* e = getenv("SAIL_HIPRTC")) path = e;
+    else path = std::string(getenv("ROCM_PATH") ? getenv("ROCM_PATH") : "/opt/rocm") + "/lib/libhiprtc.so.7";
+    void* h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* d = dlerror();
+      why = "dlmopen " + path + ": " + (d ? d : "?");
+    } else {
+      r.create = (decltype(r.create))dlsym(h, "hiprtcCreateProgram");
+      r.compile = (decltype(r.compile))dlsym(h, "hiprtcCompileProgram");
+      r.logSize = (decltype(r.logSize))dlsym(h, "hiprtcGetProgramLogSize");
+      r.log = (decltype(r.log))dlsym(h, "hiprtcGetProgramLog");
+      r.codeSize = (decltype(r.codeSize))dlsym(h, "hiprtcGetCodeSize");
+      r.code = (decltype(r.code))dlsym(h, "hiprtcGetCode");
+      r.destroy = (decltype(r.destroy))dlsym(h, "hiprtcDestroyProgram");
+      r.errStr = (decltype(r.errStr))dlsym(h, "hiprtcGetErrorString");
+      ok = r.create && r.compile && r.logSize && r.log && r.codeSize && r.code && r.destroy && r.errStr;
+      if (!ok) why = path + ": missing hipRTC entry points";
+    }
+  }
+  if (!ok) { err = why; return nullptr; }
+  return &r;
+}
+
 // the same floating-point contract as sail_amd/build.sh: no contraction, no fast math, no SLP packing
 int compile(const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
   char defs[512];
@@ -48,28 +96,29 @@ int compile(const std::string& arch, const Key& k, std::vector<char>& code, std:
            "#define SAIL_JIT_KS 0x%xu\n#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n"
            "#define SAIL_JIT_NT %d\n#include \"sail_trace.hip\"\n",
            kWaves[k.mode], k.mode == 1, k.mode == 2, k.ks, k.km, k.kt, k.kl, kThreads[k.mode]);
+  const Rtc* R = rtc(err);
+  if (!R) return -1;
   hiprtcProgram prog;
-  hiprtcResult r = hiprtcCreateProgram(&prog, defs, "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts,
-                                       sail_jit_src_names);
-  if (r != HIPRTC_SUCCESS) { err = hiprtcGetErrorString(r); return -1; }
+  hiprtcResult r = R->create(&prog, defs, "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts, sail_jit_src_names);
+  if (r != HIPRTC_SUCCESS) { err = R->errStr(r); return -1; }
   const std::string archOpt = "--offload-arch=" + arch;
   const char* opts[] = {archOpt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                         "-mllvm", "-vectorize-slp=false"};
-  r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  r = R->compile(prog, (int)(sizeof opts / sizeof opts[0]), opts);
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
+    R->logSize(prog, &n);
     std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    err = std::string(hiprtcGetErrorString(r)) + ": " + log.substr(0, 2000);
-    hiprtcDestroyProgram(&prog);
+    if (n) R->log(prog, &log[0]);
+    err = std::string(R->errStr(r)) + ": " + log.substr(0, 2000);
+    R->destroy(&prog);
     return -1;
   }
   size_t n = 0;
-  hiprtcGetCodeSize(prog, &n);
+  R->codeSize(prog, &n);
   code.resize(n);
-  hiprtcGetCode(prog, code.data());
-  hiprtcDestroyProgram(&prog);
+  R->code(prog, code.data());
+  R->destroy(&prog);
   return n ? 0 : -1;
 }
 

@@ -14,6 +14,14 @@ from sail_amd import capi
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
+def _torch_runtime_loaded():
+    """PyTorch-ROCm brings its own HIP runtime, hipRTC and comgr (an older ROCm, same sonames). Importing it first is
+    the common case in a process that uses this library, and the run-time kernels must not depend on it."""
+    import torch  # noqa: F401
+    maps = open("/proc/self/maps").read()
+    return "torch/lib/libhiprtc" in maps or "torch/lib/libamdhip64" in maps
+
+
 def _compile(masks, cull):
     lib = capi.load()
     pl = capi.Plugins(*masks)
@@ -55,6 +63,7 @@ def product_kernels(tmp_path_factory):
 
 
 def test_all_plugin_jit_equals_precompiled_generic(tmp_path, product_kernels):
+    assert _torch_runtime_loaded()  # the library's own toolchain compiles anyway (sail_jit.cpp: dlmopen)
     code = _compile([0xFFFFFFFF] * 4, 0)
     p = tmp_path / "jit.co"
     p.write_bytes(code)

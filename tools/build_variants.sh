@@ -18,6 +18,6 @@ while [ $# -ge 2 ]; do
   case "$flags" in src=*) src=${flags%% *}; src=${src#src=}; flags=${flags#src=$src}; esac
   $HIPCC $COMMON $flags -Icsrc -c csrc/$src -o build/variants/trace_$name.o
   $HIPCC -shared -fPIC --offload-arch=gfx950 build/variants/trace_$name.o build/variants/sail_capi.o \
-    build/variants/sail_hostmath.o build/variants/sail_jit.o build/variants/sail_jit_src.o -o lib/variants/libsail_hip_$name.so -ldl -lhiprtc
+    build/variants/sail_hostmath.o build/variants/sail_jit.o build/variants/sail_jit_src.o -o lib/variants/libsail_hip_$name.so -ldl
   echo "built $name ($flags)"
 done

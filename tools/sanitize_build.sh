@@ -19,7 +19,7 @@ for f in sail_capi sail_hostmath sail_jit; do
 done
 $HIPCC -shared -fPIC -shared-libasan -fsanitize=address,undefined -fno-gpu-sanitize --offload-arch=gfx950 \
   sail_amd/build/sail_trace.o $OUT/sail_capi.o $OUT/sail_hostmath.o $OUT/sail_jit.o sail_amd/build/sail_jit_src.o \
-  -o $OUT/libsail_hip_asan.so -ldl -lhiprtc
+  -o $OUT/libsail_hip_asan.so -ldl
 $CLANG -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math $SAN oracle/sail_oracle.cpp \
   -o $OUT/libsail_oracle_asan.so
 if [ -d /usr/include/node ]; then

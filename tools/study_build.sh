@@ -22,6 +22,6 @@ for name in "$@"; do
   wait
   for o in sail_trace sail_capi sail_hostmath sail_jit sail_jit_src; do [ -s $d/$o.o ] || { echo "study $name: $o failed"; exit 1; }; done
   $HIPCC -shared -fPIC --offload-arch=gfx950 $d/sail_trace.o $d/sail_capi.o $d/sail_hostmath.o $d/sail_jit.o \
-    $d/sail_jit_src.o -o sail_amd/lib/variants/libsail_hip_$name.so -ldl -lhiprtc
+    $d/sail_jit_src.o -o sail_amd/lib/variants/libsail_hip_$name.so -ldl
   echo "built $name"
 done
