@@ -121,7 +121,7 @@ enum sail_debug_option {
    * per-scene program, src/scene/scene.js:70-112), a sum of bits: 1 flat-path scenes (fewer than
    * SAIL_DEBUG_CULL_MIN_PRIMS primitives) that the precompiled Cornell and room kernels do not cover, 8 those as a
    * room-family kernel (SAIL_JIT_MODE_ROOM) instead of a plain one, 4 scenes of the room kernel's set, 2 pre-cull-path
-   * scenes. 0: the precompiled kernels only. Same results [1] */
+   * scenes. 0: the precompiled kernels only. Same results [11 = 1 + 2 + 8; measured in profiles/r04_jit_forms.jsonl] */
   SAIL_DEBUG_JIT = 9
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);

@@ -147,7 +147,7 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int jit = 1;           // SAIL_DEBUG_JIT bits: which scenes get a kernel compiled for their plugin set (jitKernels)
+  int jit = 11;          // SAIL_DEBUG_JIT bits: which scenes get a kernel compiled for their plugin set (jitKernels)
   bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
   std::string jitError;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)

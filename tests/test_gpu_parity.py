@@ -651,8 +651,10 @@ def test_jit_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
     out = {}
     one = {capi.DEBUG_SAMPLE_GROUPS: 1}  # a small frame would otherwise split its samples into groups
-    room = {capi.DEBUG_JIT: 1 | 8}  # the same scenes in the room kernel's form (SAIL_JIT_MODE_ROOM)
-    for label, dbg in (("jit", one), ("jit_groups", {capi.DEBUG_SAMPLE_GROUPS: 2}), ("generic", {capi.DEBUG_JIT: 0, **one}),
+    plain = {capi.DEBUG_JIT: 1}  # the all-plugin kernel's form (SAIL_JIT_MODE_FLAT)
+    room = {capi.DEBUG_JIT: 1 | 8}  # the room kernel's form (SAIL_JIT_MODE_ROOM, the default)
+    for label, dbg in (("jit", {**plain, **one}), ("jit_groups", {**plain, capi.DEBUG_SAMPLE_GROUPS: 2}),
+                       ("generic", {capi.DEBUG_JIT: 0, **one}),
                        ("jit_room", {**room, **one}), ("jit_room_groups", {**room, capi.DEBUG_SAMPLE_GROUPS: 3})):
         ctx = capi.Context(W, H, debug=dbg)
         try:
