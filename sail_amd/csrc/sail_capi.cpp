@@ -16,6 +16,7 @@
 
 // launch wrappers defined next to the kernels (sail_trace.hip)
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
+extern const int sail_trace_phase_timing;  // sail_trace.hip: 1 in the phase-timing build (libsail_hip_phase.so)
 // sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
 int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, hipFunction_t* plain,
                      hipFunction_t* grouped, std::string* err);
@@ -147,7 +148,7 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int jit = 11;          // SAIL_DEBUG_JIT bits: which scenes get a kernel compiled for their plugin set (jitKernels)
+  int jit = sail_trace_phase_timing ? 0 : 11;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels)
   bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
   std::string jitError;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)

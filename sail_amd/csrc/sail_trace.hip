@@ -2403,6 +2403,8 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
   out[i] = r;
 }
 
+// the phase-timing build's contexts keep to these (instrumented) kernels: no run-time compiled ones (sail_capi.cpp)
+extern const int sail_trace_phase_timing = SAIL_PHASE_TIMING;
 #if SAIL_PHASE_TIMING
 // phase-timing readout for the variant harness (tools/variant_bench.py --phases)
 extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
