@@ -146,15 +146,16 @@ def ops_per_segment(sc, masks, mvp, W, H, B):
     return ops / max(segs, 1), oracle.ops_live() / max(segs, 1)
 
 
-def profiled_traffic(workload, px, spp, bounces):
-    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same workload and
-    launch shape (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary*.json); None if none matches."""
+def profiled_traffic(workload, px, spp, bounces, kernel):
+    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same workload, launch shape
+    and trace kernel (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary*.json); None if none matches."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
         L = rec.get("launch", {})
-        if rec.get("workload", "cornell_box_readme_C2") == workload and L.get("pixels") == px and L.get("spp") == spp and L.get("bounces") == bounces:
+        if (rec.get("workload", "cornell_box_readme_C2") == workload and L.get("pixels") == px and L.get("spp") == spp
+                and L.get("bounces") == bounces and rec.get("kernel") == kernel):
             return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT), rec
     return None, None, None
 
@@ -373,7 +374,7 @@ def main():
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         achieved_live = ops_live * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
-        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B)
+        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B, ctx.kernel_name())
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
