@@ -121,7 +121,8 @@ enum sail_debug_option {
    * per-scene program, src/scene/scene.js:70-112), a sum of bits: 1 flat-path scenes (fewer than
    * SAIL_DEBUG_CULL_MIN_PRIMS primitives) that the precompiled Cornell and room kernels do not cover, 8 those as a
    * room-family kernel (SAIL_JIT_MODE_ROOM) instead of a plain one, 4 scenes of the room kernel's set, 2 pre-cull-path
-   * scenes. 0: the precompiled kernels only. Same results [11 = 1 + 2 + 8; measured in profiles/r04_jit_forms.jsonl] */
+   * scenes, 16 every flat-path scene of at most 8 primitives compiled for its rows too (their count and shape types).
+   * 0: the precompiled kernels only. Same results [11 = 1 + 2 + 8; measured in profiles/r04_jit_forms.jsonl] */
   SAIL_DEBUG_JIT = 9
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
@@ -186,7 +187,10 @@ enum sail_jit_mode {
   SAIL_JIT_MODE_CULL = 1, /* pre-cull path (1,024-thread workgroups) */
   SAIL_JIT_MODE_ROOM = 2  /* flat path, the room kernel's form (7 waves, two-barrier sort, first sample group at home) */
 };
-int sail_jit_compile(const sail_plugins* plugins, int mode, void* code, size_t* bytes);
+/* rows > 0 (at most 8, flat forms only): compile for a scene of exactly these rows, row_types[i] = the shape id of row i
+ * (SAIL_CUBE ..., each in plugins->shape_mask): the primitive sweeps become straight-line code over the rows */
+int sail_jit_compile(const sail_plugins* plugins, int mode, const int32_t* row_types, int rows, void* code,
+                     size_t* bytes);
 
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */
 /* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):

@@ -132,7 +132,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_accum_parts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
         "sail_save_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.POINTER(ctypes.c_uint64)]),
         "sail_load_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.c_uint64]),
-        "sail_jit_compile": (ctypes.c_int, [ctypes.POINTER(Plugins), ctypes.c_int, vp, ctypes.POINTER(ctypes.c_size_t)]),
+        "sail_jit_compile": (ctypes.c_int, [ctypes.POINTER(Plugins), ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                            vp, ctypes.POINTER(ctypes.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -18,10 +18,7 @@
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
 extern const int sail_trace_phase_timing;  // sail_trace.hip: 1 in the phase-timing build (libsail_hip_phase.so)
 // sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
-int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, hipFunction_t* plain,
-                     hipFunction_t* grouped, std::string* err);
-int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, void* code,
-                  size_t* bytes, std::string* err);
+#include "sail_jit.h"
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
 hipError_t sail_launch_accum(const SailTraceArgs& A, int blocks, hipStream_t s);
 hipError_t sail_launch_math(int fn, const float* x, const float* y, float* out, int count);
@@ -153,6 +150,7 @@ struct sail_ctx {
   std::string jitError;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
   int lastJitMode = 0;
+  std::vector<int> primTypes;  // decoded shape id of each row (run-time kernels compiled for the scene's rows)
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
   int numCUs = 256;
@@ -243,27 +241,50 @@ int kernelSetFor(const sail_ctx* c) {
 
 // the sample-group stage's cap (12 B per owned pixel per staged sample): 8 GiB
 constexpr size_t kStageCapBytes = (size_t)8 << 30;
+// Launch bounds of a run-time kernel by form and by the precompiled family its plugin set falls in: the precompiled
+// kernels' own (6 waves all-plugin, 8 Cornell, 7 room, 8 pre-cull), except that a flat scene outside the Cornell and room
+// sets compiled in the room form runs at 8 waves (its smaller kernel spills less: ALL +3.6 %, AREA +3.8 % over 7,
+// profiles/r04_jit_occupancy.jsonl).
+int jitWaves(int mode, int kernelSet) {
+  if (mode == SAIL_JIT_MODE_CULL) return 8;
+  if (mode == SAIL_JIT_MODE_ROOM) return kernelSet == SAIL_KSET_ROOM ? 7 : 8;
+  return kernelSet == SAIL_KSET_CORNELL ? 8 : 6;
+}
 // SAIL_DEBUG_JIT bits (include/sail_hip.h): 1 flat scenes outside the Cornell and room sets, 2 pre-cull scenes, 4 room-set
-// scenes (room family), 8 the flat scenes of bit 1 as room family.
+// scenes, 8 the flat scenes of bit 1 in the room form, 16 flat scenes compiled for their rows as well (any flat scene).
 bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* mode) {
   if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric) return false;
   const int set = kernelSetFor(c);
+  const bool rows = (c->jit & 16) && c->n >= 1 && c->n <= kSailJitMaxRows && c->n < c->cullMinPrims &&
+                    (int)c->primTypes.size() == c->n;
   int m;
   if (set == SAIL_KSET_GENERIC && c->n >= c->cullMinPrims) {
     if (!(c->jit & 2)) return false;
     m = SAIL_JIT_MODE_CULL;
   } else if (set == SAIL_KSET_GENERIC) {
-    if (!(c->jit & 1)) return false;
+    if (!(c->jit & 1) && !rows) return false;
     m = (c->jit & 8) ? SAIL_JIT_MODE_ROOM : SAIL_JIT_MODE_FLAT;
   } else if (set == SAIL_KSET_ROOM) {
-    if (!(c->jit & 4)) return false;
+    if (!(c->jit & 4) && !rows) return false;
     m = SAIL_JIT_MODE_ROOM;
   } else {
-    return false;  // the Cornell kernel's set is the Cornell box's own
+    if (!rows) return false;  // the Cornell kernel's set is the Cornell box's own
+    m = SAIL_JIT_MODE_FLAT;
   }
   const sail_plugins& p = c->plugins;
+  SailJitSpec spec;
+  spec.ks = p.shape_mask; spec.km = p.material_mask; spec.kt = p.texture_mask; spec.kl = p.light_mask;
+  spec.mode = m;
+  spec.waves = jitWaves(m, set);
+  if (rows && m != SAIL_JIT_MODE_CULL) {
+    spec.rows = c->n;
+    for (int i = 0; i < c->n; i++) spec.types[i] = c->primTypes[i];
+    for (int i = 0; i < c->n; i++)
+      if (spec.types[i] < 1 || !((spec.ks >> spec.types[i]) & 1u)) spec.rows = 0;  // a row no compiled shape hits
+    if (!spec.rows) for (int& t : spec.types) t = 0;
+  }
   std::string err;
-  if (sail_jit_kernels(c->device, p.shape_mask, p.material_mask, p.texture_mask, p.light_mask, m, plain, grouped, &err)) {
+  if (sail_jit_kernels(c->device, spec, plain, grouped, &err)) {
     c->jitFailed = true;
     c->jitError = err;
     return false;
@@ -1132,6 +1153,8 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   decodePrims(objects, n, tn, plugins->shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, texparams, tn);
   c->primExtent = primExtent(prims);
+  c->primTypes.clear();
+  for (const SailPrim& q : prims) c->primTypes.push_back(q.type);
   // per light row: the geometry row an AreaLight samples (area.glsl:8 + shader.shape.js:56)
   std::vector<int32_t> lrow((size_t)(ln > 0 ? ln : 1), 0);
   TexView lv{lights, 18, ln};
@@ -1180,6 +1203,8 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   decodePrims(objects, n, c->tn, c->plugins.shape_mask, prims, &c->shadowAnyHit, &c->scene);
   fillCats(prims, c->tpRows.data(), c->tn);
   c->primExtent = primExtent(prims);
+  c->primTypes.clear();
+  for (const SailPrim& q : prims) c->primTypes.push_back(q.type);  // a kernel compiled for the rows follows them
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1624,11 +1649,27 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
   return SAIL_OK;
 }
 
-int sail_jit_compile(const sail_plugins* plugins, int mode, void* code, size_t* bytes) {
-  if (!plugins || !bytes || mode < SAIL_JIT_MODE_FLAT || mode > SAIL_JIT_MODE_ROOM) return SAIL_E_INVALID;
+int sail_jit_compile(const sail_plugins* plugins, int mode, const int32_t* row_types, int rows, void* code,
+                     size_t* bytes) {
+  if (!plugins || !bytes || mode < SAIL_JIT_MODE_FLAT || mode > SAIL_JIT_MODE_ROOM || rows < 0 ||
+      rows > kSailJitMaxRows || (rows > 0 && !row_types))
+    return SAIL_E_INVALID;
+  // the plugin set's precompiled family, as kernelSetFor decides it for a flat scene of these masks
+  const sail_plugins& p = *plugins;
+  int set = SAIL_KSET_GENERIC;
+  if ((p.shape_mask & ~SAIL_KSET_CORNELL_SHAPES) == 0 && (p.material_mask & ~SAIL_KSET_CORNELL_MATS) == 0 &&
+      (p.texture_mask & ~SAIL_KSET_CORNELL_TEX) == 0 && p.light_mask == 0)
+    set = SAIL_KSET_CORNELL;
+  else if ((p.shape_mask & ~SAIL_KSET_ROOM_SHAPES) == 0)
+    set = SAIL_KSET_ROOM;
+  SailJitSpec spec;
+  spec.ks = p.shape_mask; spec.km = p.material_mask; spec.kt = p.texture_mask; spec.kl = p.light_mask;
+  spec.mode = mode;
+  spec.waves = jitWaves(mode, mode == SAIL_JIT_MODE_CULL ? SAIL_KSET_GENERIC : set);
+  spec.rows = rows;
+  for (int i = 0; i < rows; i++) spec.types[i] = row_types[i];
   std::string err;
-  if (sail_jit_code("gfx950", plugins->shape_mask, plugins->material_mask, plugins->texture_mask, plugins->light_mask,
-                    mode, code, bytes, &err))
+  if (sail_jit_code("gfx950", spec, code, bytes, &err))
     return fail(nullptr, SAIL_E_INVALID, "sail_jit_compile: %s", err.c_str());
   return SAIL_OK;
 }

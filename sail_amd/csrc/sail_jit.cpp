@@ -26,26 +26,28 @@
 #include <tuple>
 #include <vector>
 
+#include "sail_jit.h"
+
 extern const char* const sail_jit_src_names[];
 extern const char* const sail_jit_src_texts[];
 extern const int sail_jit_src_count;
 
 namespace {
 
-// mode: 0 flat (the all-plugin kernel's form), 1 pre-cull, 2 flat in the room kernel's form (sail_hip.h sail_jit_mode)
 struct Key {
-  uint32_t ks, km, kt, kl;
-  int mode;
+  SailJitSpec s;
   bool operator<(const Key& o) const {
-    return std::tie(ks, km, kt, kl, mode) < std::tie(o.ks, o.km, o.kt, o.kl, o.mode);
+    const auto t = [](const SailJitSpec& x) {
+      return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.types[0], x.types[1], x.types[2], x.types[3],
+                      x.types[4], x.types[5], x.types[6], x.types[7]);
+    };
+    return t(s) < t(o.s);
   }
 };
-// launch bounds of each form: the precompiled kernels' (sail_trace.hip SAIL_*_WAVES / _NT)
-constexpr int kWaves[3] = {6, 8, 7}, kThreads[3] = {256, 1024, 256};
 std::mutex g_jitMutex;
-std::map<std::pair<std::string, Key>, std::vector<char>> g_code;  // (arch, plugin set) -> code object
+std::map<std::pair<std::string, Key>, std::vector<char>> g_code;  // (arch, spec) -> code object
 struct Loaded { hipModule_t mod; hipFunction_t plain, grouped; };
-std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, plugin set) -> module
+std::map<std::pair<int, Key>, Loaded> g_loaded;                  // (device, spec) -> module
 
 // hipRTC entry points from the toolchain's library (SAIL_HIPRTC, else $ROCM_PATH or /opt/rocm, lib/libhiprtc.so.7)
 struct Rtc {
@@ -90,12 +92,16 @@ const Rtc* rtc(std::string& err) {  // under g_jitMutex
 
 // the same floating-point contract as sail_amd/build.sh: no contraction, no fast math, no SLP packing
 int compile(const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
-  char defs[512];
+  const SailJitSpec& sp = k.s;
+  std::string types;
+  for (int i = 0; i < sp.rows; i++) types += (i ? ", " : "") + std::to_string(sp.types[i]);
+  char defs[768];
   snprintf(defs, sizeof defs,
            "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %d\n#define SAIL_JIT_FAM %d\n"
            "#define SAIL_JIT_KS 0x%xu\n#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n"
-           "#define SAIL_JIT_NT %d\n#include \"sail_trace.hip\"\n",
-           kWaves[k.mode], k.mode == 1, k.mode == 2, k.ks, k.km, k.kt, k.kl, kThreads[k.mode]);
+           "#define SAIL_JIT_NT %d\n#define SAIL_JIT_N %d\n#define SAIL_JIT_TYPES %s\n#include \"sail_trace.hip\"\n",
+           sp.waves, sp.mode == 1, sp.mode == 2, sp.ks, sp.km, sp.kt, sp.kl, sp.mode == 1 ? 1024 : 256, sp.rows,
+           sp.rows ? types.c_str() : "0");
   const Rtc* R = rtc(err);
   if (!R) return -1;
   hiprtcProgram prog;
@@ -122,14 +128,20 @@ int compile(const std::string& arch, const Key& k, std::vector<char>& code, std:
   return n ? 0 : -1;
 }
 
+bool validSpec(const SailJitSpec& sp, std::string* err) {
+  bool ok = sp.mode >= 0 && sp.mode <= 2 && sp.waves >= 1 && sp.waves <= 8 && sp.rows >= 0 && sp.rows <= kSailJitMaxRows &&
+            !(sp.mode == 1 && sp.rows);  // the pre-cull kernels sweep candidates, not rows
+  for (int i = 0; ok && i < sp.rows; i++) ok = sp.types[i] >= 1 && sp.types[i] <= 9 && ((sp.ks >> sp.types[i]) & 1u);
+  if (!ok) *err = "invalid kernel specialisation";
+  return ok;
+}
 }  // namespace
 
-// The trace kernel pair (ungrouped, _grouped) for exactly this plugin set on `device` (the current device), compiled
-// on first use. Returns 0 and the functions, or -1 with a message (the caller then runs the precompiled kernel).
-int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, hipFunction_t* plain,
-                     hipFunction_t* grouped, std::string* err) {
-  if (mode < 0 || mode > 2) { *err = "unknown kernel form"; return -1; }
-  const Key k{ks, km, kt, kl, mode};
+// The trace kernel pair (ungrouped, _grouped) for `spec` on `device` (the current device), compiled on first use.
+// Returns 0 and the functions, or -1 with a message (the caller then runs the precompiled kernel).
+int sail_jit_kernels(int device, const SailJitSpec& spec, hipFunction_t* plain, hipFunction_t* grouped, std::string* err) {
+  if (!validSpec(spec, err)) return -1;
+  const Key k{spec};
   std::lock_guard<std::mutex> lock(g_jitMutex);
   auto it = g_loaded.find({device, k});
   if (it == g_loaded.end()) {
@@ -143,7 +155,7 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
     if (code.empty() && compile(arch, k, code, *err)) { g_code.erase({arch, k}); return -1; }
     Loaded L{};
     if (hipModuleLoadData(&L.mod, code.data()) != hipSuccess) { *err = "hipModuleLoadData"; return -1; }
-    const char* fn = k.mode == 1 ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
+    const char* fn = spec.mode == 1 ? "sail_trace_kernel_cull_jit" : "sail_trace_kernel_jit";
     if (hipModuleGetFunction(&L.plain, L.mod, fn) != hipSuccess ||
         hipModuleGetFunction(&L.grouped, L.mod, (std::string(fn) + "_grouped").c_str()) != hipSuccess) {
       (void)hipModuleUnload(L.mod);
@@ -157,13 +169,12 @@ int sail_jit_kernels(int device, uint32_t ks, uint32_t km, uint32_t kt, uint32_t
   return 0;
 }
 
-// Host-only: the code object of the plugin set's kernel pair for `arch`, compiled (not loaded) by the same path
+// Host-only: the code object of `spec`'s kernel pair for `arch`, compiled (not loaded) by the same path
 // (include/sail_hip.h sail_jit_compile). *bytes = its size; copied into `code` when `code` is not null and the
 // buffer (*bytes on entry) is large enough.
-int sail_jit_code(const char* arch, uint32_t ks, uint32_t km, uint32_t kt, uint32_t kl, int mode, void* code,
-                  size_t* bytes, std::string* err) {
-  if (mode < 0 || mode > 2) { *err = "unknown kernel form"; return -1; }
-  const Key k{ks, km, kt, kl, mode};
+int sail_jit_code(const char* arch, const SailJitSpec& spec, void* code, size_t* bytes, std::string* err) {
+  if (!validSpec(spec, err)) return -1;
+  const Key k{spec};
   std::lock_guard<std::mutex> lock(g_jitMutex);
   auto& c = g_code[{arch, k}];
   if (c.empty() && compile(arch, k, c, *err)) { g_code.erase({arch, k}); return -1; }

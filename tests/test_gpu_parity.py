@@ -709,6 +709,32 @@ def test_jit_room_set_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
         assert bit_equal(got, want).all(), dbg
 
 
+@pytest.mark.parametrize("name,W,H,spp,B", [("C1", 40, 24, 3, 6), ("C3", 40, 36, 3, 6), ("UI", 36, 28, 3, 5),
+                                            ("ALL", 40, 32, 3, 6), ("BILERP", 33, 17, 2, 5), ("N1S", 24, 20, 2, 4)])
+def test_jit_row_specialised_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B):
+    """SAIL_DEBUG_JIT bit 16: a flat scene compiled for its rows (count and shape types as constants: straight-line
+    sweeps) in its family's form -- Cornell, room, or room form for the rest; bit-exact against the oracle, ungrouped
+    and in 3 sample groups, and again after sail_update_objects moves the rows (same types: the same kernel)"""
+    sc = fixtures["scenes"][name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    for groups in (1, 3):
+        ctx = capi.Context(W, H, debug={capi.DEBUG_JIT: 11 | 16, capi.DEBUG_SAMPLE_GROUPS: groups})
+        try:
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            got = ctx.read_accum()
+            assert ctx.kernel_name().startswith("sail_trace_kernel_jit"), ctx.kernel_name()
+            assert bit_equal(got, want).all(), groups
+            if groups == 3:
+                rows = np.ascontiguousarray(np.asarray(sc["objects"], np.float32).reshape(-1))
+                assert ctx.lib.sail_update_objects(ctx.h, capi._ptr(rows), sc["n"]) == 0  # Renderer.updateObjects
+                ctx.render_schedule(inv, seeds, sc["eye"], B)
+                assert bit_equal(ctx.read_accum(), want).all()
+        finally:
+            ctx.close()
+
+
 def test_jit_precull_kernel_bit_exact(gpu, fixtures):
     """SAIL_DEBUG_JIT bit 2: the pre-cull path (C4, 67 rows) compiled for exactly its plugin set, 1,024-thread
     workgroups like the precompiled pre-cull kernel; bit-exact against the oracle, with and without sample groups"""

@@ -22,15 +22,16 @@ def _torch_runtime_loaded():
     return "torch/lib/libhiprtc" in maps or "torch/lib/libamdhip64" in maps
 
 
-def _compile(masks, cull):
+def _compile(masks, mode, rows=()):
     lib = capi.load()
     pl = capi.Plugins(*masks)
+    types = (ctypes.c_int32 * max(len(rows), 1))(*rows)
     n = ctypes.c_size_t(0)
-    assert lib.sail_jit_compile(ctypes.byref(pl), cull, None, ctypes.byref(n)) == 0, lib.sail_last_error(None)
+    assert lib.sail_jit_compile(ctypes.byref(pl), mode, types, len(rows), None, ctypes.byref(n)) == 0, lib.sail_last_error(None)
     buf = ctypes.create_string_buffer(n.value)
-    assert lib.sail_jit_compile(ctypes.byref(pl), cull, buf, ctypes.byref(n)) == 0
+    assert lib.sail_jit_compile(ctypes.byref(pl), mode, types, len(rows), buf, ctypes.byref(n)) == 0
     small = ctypes.c_size_t(16)
-    assert lib.sail_jit_compile(ctypes.byref(pl), cull, buf, ctypes.byref(small)) != 0  # too small a buffer
+    assert lib.sail_jit_compile(ctypes.byref(pl), mode, types, len(rows), buf, ctypes.byref(small)) != 0  # too small
     return buf.raw
 
 
@@ -97,8 +98,45 @@ def test_room_form_of_the_room_set_equals_precompiled_room_kernel(tmp_path, prod
     assert jit["sail_trace_kernel_jit_grouped"] == product_kernels["sail_trace_kernel_room_grouped"]
 
 
-def test_unknown_mode_refused():
+def test_cornell_set_flat_form_equals_precompiled_cornell_kernel(tmp_path, fixtures, product_kernels):
+    """the flat form for the Cornell box's plugin set runs at the Cornell kernel's 8 waves: the same kernel pair"""
+    code = _compile(capi.plugin_masks(fixtures["scenes"]["C1"]["plugins"]), 0)
+    p = tmp_path / "jit.co"
+    p.write_bytes(code)
+    jit = _kernels(_disasm(str(p)))
+    assert jit["sail_trace_kernel_jit"] == product_kernels["sail_trace_kernel_cornell"]
+    assert jit["sail_trace_kernel_jit_grouped"] == product_kernels["sail_trace_kernel_cornell_grouped"]
+
+
+@pytest.mark.parametrize("scene,mode", [("C1", 0), ("C3", 2), ("ALL", 2)])
+def test_row_specialised_kernel_has_no_row_loop(tmp_path, fixtures, scene, mode):
+    """compiled for the scene's rows (count and shape types), the kernel differs from the plugin-set-only one and
+    still compiles to the same kernel names"""
+    sc = fixtures["scenes"][scene]
+    masks = capi.plugin_masks(sc["plugins"])
+    types = [capi._SHAPES[b["shape"].lower()] for b in sc["boundbox"]]
+    code = _compile(masks, mode, types)
+    p = tmp_path / "jit.co"
+    p.write_bytes(code)
+    jit = _kernels(_disasm(str(p)))
+    plain = _kernels(_disasm_bytes(tmp_path, _compile(masks, mode)))
+    assert set(jit) == {"sail_trace_kernel_jit", "sail_trace_kernel_jit_grouped"}
+    assert jit["sail_trace_kernel_jit"] != plain["sail_trace_kernel_jit"]
+
+
+def _disasm_bytes(tmp_path, code):
+    q = tmp_path / "plain.co"
+    q.write_bytes(code)
+    return _disasm(str(q))
+
+
+def test_bad_specialisations_refused(fixtures):
     lib = capi.load()
-    pl = capi.Plugins(1, 1, 0, 0)
     n = ctypes.c_size_t(0)
-    assert lib.sail_jit_compile(ctypes.byref(pl), 3, None, ctypes.byref(n)) != 0
+    pl = capi.Plugins(*capi.plugin_masks(fixtures["scenes"]["C1"]["plugins"]))
+    none = (ctypes.c_int32 * 1)(0)
+    assert lib.sail_jit_compile(ctypes.byref(pl), 3, none, 0, None, ctypes.byref(n)) != 0       # unknown form
+    rect = (ctypes.c_int32 * 1)(3)                                                             # Rectangle: not compiled in
+    assert lib.sail_jit_compile(ctypes.byref(pl), 0, rect, 1, None, ctypes.byref(n)) != 0
+    assert lib.sail_jit_compile(ctypes.byref(pl), 1, (ctypes.c_int32 * 1)(1), 1, None, ctypes.byref(n)) != 0  # pre-cull
+    assert lib.sail_jit_compile(ctypes.byref(pl), 0, (ctypes.c_int32 * 9)(*[1] * 9), 9, None, ctypes.byref(n)) != 0
