@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Per-phase wave-time attribution of the trace kernel from a -DSAIL_PHASE_TIMING=1 build
-(tools/build_variants.sh ph "-DSAIL_PHASE_TIMING=1"). Each wave accumulates s_memtime deltas between
-convergence points of the bounce loop; the shares are of summed wave time (all waves, all launches).
-Usage: tools/phase_profile.py sail_amd/lib/variants/libsail_hip_ph.so [C1 C3 C4]"""
+(sail_amd/build.sh builds it as sail_amd/lib/libsail_hip_phase.so). Each wave accumulates s_memtime deltas between
+convergence points of the bounce loop; the shares are of summed wave time (all waves, all launches). "sort + barriers"
+is the path sort between the sweep and the hit record (LDS counts, scan, scatter, gather and the barriers' waits);
+a sample's end (radiance read-back, accumulation or staging) falls into the next sample's "sweep". Round-4 files
+before this note called the sort phase "accumulate".
+Usage: tools/phase_profile.py sail_amd/lib/libsail_hip_phase.so [C1 C3 C4]"""
 import ctypes
 import json
 import os
@@ -14,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from sail_amd import capi  # noqa: E402
 
-PHASES = ["sweep", "hit record", "shading frame", "hash RNG", "BSDF sample", "light + shadow", "next ray", "accumulate"]
+PHASES = ["sweep", "hit record", "shading frame", "hash RNG", "BSDF sample", "light + shadow", "next ray", "sort + barriers"]
 
 
 def main():
