@@ -249,7 +249,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--launch-spp", type=int, default=32)
+    ap.add_argument("--launch-spp", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c1-full", action="store_true", help="skip the ~30 s full C1 render of the CPU baseline")
     ap.add_argument("--force-rccl", action="store_true",

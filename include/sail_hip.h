@@ -98,7 +98,7 @@ int sail_update_objects(sail_ctx* ctx, const float* objects, int n);
 
 int sail_set_accum_mode(sail_ctx* ctx, int mode);        /* resets accumulation */
 int sail_set_partition(sail_ctx* ctx, int rank, int world, int mode);
-int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch (default 32) */
+int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch (default 64) */
 /* Test / study switches (no reference counterpart; none changes a result, which the parity suite checks).
  * The product's defaults are the values in brackets. */
 enum sail_debug_option {
@@ -122,7 +122,7 @@ enum sail_debug_option {
    * SAIL_DEBUG_CULL_MIN_PRIMS primitives) that the precompiled Cornell and room kernels do not cover, 8 those as a
    * room-family kernel (SAIL_JIT_MODE_ROOM) instead of a plain one, 4 scenes of the room kernel's set, 2 pre-cull-path
    * scenes, 16 every flat-path scene of at most 8 primitives compiled for its rows too (their count and shape types).
-   * 0: the precompiled kernels only. Same results [11 = 1 + 2 + 8; measured in profiles/r04_jit_forms.jsonl] */
+   * 0: the precompiled kernels only. Same results [27 = 1 + 2 + 8 + 16; measured in profiles/r04_jit_*.jsonl] */
   SAIL_DEBUG_JIT = 9
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);

@@ -145,7 +145,7 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int jit = sail_trace_phase_timing ? 0 : 11;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels)
+  int jit = sail_trace_phase_timing ? 0 : 27;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels)
   bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
   std::string jitError;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
@@ -158,7 +158,7 @@ struct sail_ctx {
   size_t stageBytes = 0;
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
-  int launchSpp = 32;
+  int launchSpp = 64;   // samples per launch: 64 measured C2 +0.7 %, C3 +0.5 %, C4/C5 +-0.2 % over 32 (profiles/r04_launch_spp*)
   uint64_t k = 0;  // global sample index of the next sample (the reference's sampleCount)
   uint64_t samplesThisRank = 0;
   uint64_t nominalSegments = 0;

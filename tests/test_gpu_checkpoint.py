@@ -224,6 +224,7 @@ def test_render_queue_bit_exact_and_batched(gpu, fixtures, devices):
     ctx = capi.Context(W, H, devices=devices) if devices else capi.Context(W, H)
     try:
         ctx.set_scene_dict(sc)
+        ctx.set_launch_samples(32)
         for s in range(spp):
             ctx.render(inv[s], sc["eye"], float(seeds[s]), B)
             if s == 9:
