@@ -3,9 +3,11 @@ the kernel sources embedded in the library with the product's floating-point fla
 kernel pair is instruction-for-instruction the precompiled all-plugin kernel pair (so the run-time path cannot differ
 in contraction, fast-math or packing), and specialised sets compile to the kernel names the contexts load."""
 import ctypes
+import os
 import re
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -140,3 +142,20 @@ def test_bad_specialisations_refused(fixtures):
     assert lib.sail_jit_compile(ctypes.byref(pl), 0, rect, 1, None, ctypes.byref(n)) != 0
     assert lib.sail_jit_compile(ctypes.byref(pl), 1, (ctypes.c_int32 * 1)(1), 1, None, ctypes.byref(n)) != 0  # pre-cull
     assert lib.sail_jit_compile(ctypes.byref(pl), 0, (ctypes.c_int32 * 9)(*[1] * 9), 9, None, ctypes.byref(n)) != 0
+
+
+def test_missing_hiprtc_is_an_error_not_a_crash(tmp_path):
+    """SAIL_HIPRTC naming a missing library: sail_jit_compile fails with the dlmopen message (contexts then keep the
+    precompiled kernels, tests/test_gpu_jit_fallback.py); a child process, as the library opens hipRTC once"""
+    child = (
+        "import ctypes, sys\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
+        "from sail_amd import capi\n"
+        "lib = capi.load(); pl = capi.Plugins(0x206, 6, 0, 0); n = ctypes.c_size_t(0)\n"
+        "rc = lib.sail_jit_compile(ctypes.byref(pl), 0, None, 0, None, ctypes.byref(n))\n"
+        "print(rc, lib.sail_last_error(None).decode())\n")
+    env = dict(os.environ, SAIL_HIPRTC=str(tmp_path / "missing" / "libhiprtc.so.7"))
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, msg = r.stdout.strip().split(" ", 1)
+    assert int(rc) != 0 and "dlmopen" in msg, r.stdout
