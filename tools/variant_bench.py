@@ -64,14 +64,15 @@ def main():
         specs = [(os.path.basename(p), p, None)
                  for p in sorted(glob.glob(os.path.join(ROOT, "sail_amd", "lib", "variants", "libsail_hip_*.so")))]
     rounds = int(os.environ.get("VARIANT_ROUNDS", "2"))  # ABCD ABCD: clock drift shows as a spread, not a bias
+    launch = int(os.environ.get("VARIANT_LAUNCH", "64"))  # samples per launch (the product default since round 4)
     ref = None
     for name, p, dbg in specs * rounds:
-        dt, ms, acc, div_bad = run(p, sc, W, H, B, spp, 32, 3, dbg)
+        dt, ms, acc, div_bad = run(p, sc, W, H, B, spp, launch, 3, dbg)
         same = ref is None or np.array_equal(acc.view(np.uint32), ref.view(np.uint32))
         if ref is None:
             ref = acc
         segs = W * H * spp * B
-        print(json.dumps({"variant": name, "scene": scene, "debug": dbg, "s": round(dt, 4), "ms_per_launch": round(ms, 3),
+        print(json.dumps({"variant": name, "scene": scene, "debug": dbg, "launch_spp": launch, "s": round(dt, 4), "ms_per_launch": round(ms, 3),
                           "Gseg_per_s": round(segs / dt / 1e9, 3), "bit_identical": bool(same), "divide_mismatches": div_bad}), flush=True)
 
 
