@@ -33,6 +33,9 @@ for step in "$@"; do
       for r in 1 2; do for cfg in C2 C3 C4; do for l in 32 64; do
         timeout -k 10 300 python bench.py --config $cfg --launch-spp $l --no-cpu-baseline --steps 1 --warmup 1 > $O/launch_${cfg}_${l}_$r.json 2> $O/launch.err || { tail $O/launch.err; exit 5; }
       done; done; done ;;
+    live_state)  # fewer live VGPRs across the sample loop (study builds segs_scalar, acc_lds)
+      for sc in C1 C3 UI ALL; do vb live_$sc 400 $sc base=main segs=$V/libsail_hip_segs_scalar.so acc=$V/libsail_hip_acc_lds.so; done
+      vb live_C4 500 C4 base=main segs=$V/libsail_hip_segs_scalar.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
