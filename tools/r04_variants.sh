@@ -36,6 +36,8 @@ for step in "$@"; do
     live_state)  # fewer live VGPRs across the sample loop (study builds segs_scalar, acc_lds)
       for sc in C1 C3 UI ALL; do vb live_$sc 400 $sc base=main segs=$V/libsail_hip_segs_scalar.so acc=$V/libsail_hip_acc_lds.so; done
       vb live_C4 500 C4 base=main segs=$V/libsail_hip_segs_scalar.so ;;
+    cull_stash)  # the pre-cull sweep without throughput / pixel in VGPRs (study build cull_stash)
+      vb stash_C4 500 C4 base=main stash=$V/libsail_hip_cull_stash.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
