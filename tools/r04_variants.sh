@@ -38,6 +38,9 @@ for step in "$@"; do
       vb live_C4 500 C4 base=main segs=$V/libsail_hip_segs_scalar.so ;;
     cull_stash)  # the pre-cull sweep without throughput / pixel in VGPRs (study build cull_stash)
       vb stash_C4 500 C4 base=main stash=$V/libsail_hip_cull_stash.so ;;
+    skip_sort1)  # no path sort at the first bounce (study build skip_sort1)
+      for sc in C1 C3 UI; do vb skip1_$sc 400 $sc base=main skip1=$V/libsail_hip_skip_sort1.so; done
+      vb skip1_C4 500 C4 base=main skip1=$V/libsail_hip_skip_sort1.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
