@@ -1697,6 +1697,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   __shared__ int sShCnt[2];
   int shph = 0;
   constexpr bool twoBar = CULL || FAM;
+  constexpr bool kSort1 = CULL || FAM;  // sort the paths at the first bounce too
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
   const TileWork tw = tileWork<GROUPED, NT>(A);
@@ -1833,6 +1834,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           sSt2[5][d] = make_float2(__int_as_float(pixel | (sw.bi << 10)), __int_as_float(key));
         }
       };
+      // the flat-form kernels (Cornell box, all-plugin) leave the first bounce unsorted: primary rays of a 16 x 4 strip
+      // mostly hit one row already and none is dead yet, so each lane keeps its own pixel's path (C1 +1.1 %; the room
+      // and pre-cull kernels keep the sort, where skipping it measured C3 -1.6 %, C4 -9.2 %:
+      // profiles/r04_skip_sort1.jsonl)
+      const bool sortNow = kSort1 || depth > 1;
+      if (sortNow) {
       if constexpr (twoBar) {
       // every wave scans the counts itself (the start of a lane's key by a cross-lane read), so no barrier
       // between the scan and the scatter; the counts alternate between two buffers, the one just read being
@@ -1866,13 +1873,16 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       __syncthreads();
       }
       alive = li < nAlive;
+      }
       ShadowPending sp;
       sp.pending = false;
       V3 eLit = v3s(0.0f);
       int keyG = 0;  // the gathered path's sort key
       PHASE_MARK(pc, 7);
       if (alive) {
-        if constexpr (kPack == 2) {
+        if (!sortNow) {
+          keyG = key;
+        } else if constexpr (kPack == 2) {
           const float4 q0 = sSt4[0][li], q1 = sSt4[1][li], q2 = sSt4[2][li];
           const int pk = __float_as_int(q2.z);
           keyG = __float_as_int(q2.w);
