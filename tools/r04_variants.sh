@@ -41,6 +41,8 @@ for step in "$@"; do
     skip_sort1)  # no path sort at the first bounce (study build skip_sort1)
       for sc in C1 C3 UI; do vb skip1_$sc 400 $sc base=main skip1=$V/libsail_hip_skip_sort1.so; done
       vb skip1_C4 500 C4 base=main skip1=$V/libsail_hip_skip_sort1.so ;;
+    cull_unroll) # the pre-cull mask build unrolled by 4 rows (study build cull_unroll)
+      vb unroll_C4 500 C4 base=main unroll=$V/libsail_hip_cull_unroll.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
