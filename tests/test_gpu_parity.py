@@ -735,6 +735,34 @@ def test_jit_row_specialised_kernel_bit_exact(gpu, fixtures, name, W, H, spp, B)
             ctx.close()
 
 
+def test_jit_row_kernel_recompiles_when_row_types_change(gpu, fixtures):
+    """sail_update_objects that changes a row's shape type (C3's Cube and first Sphere rows swapped): the context
+    compiles the kernel for the new rows at the next render, and the frame equals the oracle's for the new rows"""
+    sc = dict(fixtures["scenes"]["C3"])
+    W, H, spp, B = 36, 28, 2, 5
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    rows = np.asarray(sc["objects"], np.float32).reshape(sc["n"], 18)
+    assert int(rows[1, 0]) == 1 and int(rows[2, 0]) == 2  # Cube, Sphere
+    swapped = rows.copy()
+    swapped[[1, 2]] = rows[[2, 1]]
+    ctx = capi.Context(W, H, debug={capi.DEBUG_SAMPLE_GROUPS: 2})
+    try:
+        ctx.set_scene_dict(sc)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        first = ctx.read_accum()
+        flat = np.ascontiguousarray(swapped.reshape(-1))
+        assert ctx.lib.sail_update_objects(ctx.h, capi._ptr(flat), sc["n"]) == 0
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got = ctx.read_accum()
+        assert ctx.kernel_name().startswith("sail_trace_kernel_jit")
+    finally:
+        ctx.close()
+    masks = capi.plugin_masks(sc["plugins"])
+    assert bit_equal(first, oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B)).all()
+    sc2 = dict(sc, objects=flat.tolist())
+    assert bit_equal(got, oracle.render(sc2, masks, W, H, inv, seeds, sc["eye"], B)).all()
+
+
 def test_jit_precull_kernel_bit_exact(gpu, fixtures):
     """SAIL_DEBUG_JIT bit 2: the pre-cull path (C4, 67 rows) compiled for exactly its plugin set, 1,024-thread
     workgroups like the precompiled pre-cull kernel; bit-exact against the oracle, with and without sample groups"""
