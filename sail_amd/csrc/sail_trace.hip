@@ -901,8 +901,22 @@ D unsigned long long chunkMask(const Ctx& c, const Ray& r, const CullRay& q, int
   unsigned lo = 0u, hi = 0u;
   const float B = bound * 1.0001f + 1e-4f;
   if (FUSED) {
-    for (int j = cnt - 1; j >= 32; j--) hi = shiftInMask(hi, padHitFMask(PRIM(c, base + j), q, B));
-    for (int j = (cnt < 32 ? cnt : 32) - 1; j >= 0; j--) lo = shiftInMask(lo, padHitFMask(PRIM(c, base + j), q, B));
+    // four rows per step (their bounds requested by scalar loads together, fewer waits; C4 +1.7 %,
+    // profiles/r04_cull_unroll.jsonl), the bits shifted in the same descending order as one row per step
+    int j = cnt - 1;
+    for (; j >= 35; j -= 4) {
+      const unsigned long long m0 = padHitFMask(PRIM(c, base + j), q, B), m1 = padHitFMask(PRIM(c, base + j - 1), q, B);
+      const unsigned long long m2 = padHitFMask(PRIM(c, base + j - 2), q, B), m3 = padHitFMask(PRIM(c, base + j - 3), q, B);
+      hi = shiftInMask(shiftInMask(shiftInMask(shiftInMask(hi, m0), m1), m2), m3);
+    }
+    for (; j >= 32; j--) hi = shiftInMask(hi, padHitFMask(PRIM(c, base + j), q, B));
+    j = (cnt < 32 ? cnt : 32) - 1;
+    for (; j >= 3; j -= 4) {
+      const unsigned long long m0 = padHitFMask(PRIM(c, base + j), q, B), m1 = padHitFMask(PRIM(c, base + j - 1), q, B);
+      const unsigned long long m2 = padHitFMask(PRIM(c, base + j - 2), q, B), m3 = padHitFMask(PRIM(c, base + j - 3), q, B);
+      lo = shiftInMask(shiftInMask(shiftInMask(shiftInMask(lo, m0), m1), m2), m3);
+    }
+    for (; j >= 0; j--) lo = shiftInMask(lo, padHitFMask(PRIM(c, base + j), q, B));
     return ((unsigned long long)hi << 32) | lo;
   }
   for (int j = cnt - 1; j >= 32; j--) hi = (hi << 1) | (padHit(PRIM(c, base + j), r, bound) ? 1u : 0u);
