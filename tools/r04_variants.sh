@@ -43,6 +43,8 @@ for step in "$@"; do
       vb skip1_C4 500 C4 base=main skip1=$V/libsail_hip_skip_sort1.so ;;
     cull_unroll) # the pre-cull mask build unrolled by 4 rows (study build cull_unroll)
       vb unroll_C4 500 C4 base=main unroll=$V/libsail_hip_cull_unroll.so ;;
+    cull_unroll8) # eight rows per step instead of four (study build cull_unroll8)
+      vb unroll8_C4 500 C4 base=main unroll8=$V/libsail_hip_cull_unroll8.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
