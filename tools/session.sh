@@ -13,6 +13,7 @@
 #   variants         tools/variant_bench.py over sail_amd/lib/variants/*.so (VARIANT_ARGS: scene W H B spp ...)
 #   phases           tools/phase_profile.py with the phase-timing build (sail_amd/lib/libsail_hip_phase.so)
 #   jshost           the JS host bench (sail_amd/js/tools/bench_host.js)
+#   torchrun         bench.py under torch.distributed.run at N = 1
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=gpurun_out/${OUT:-session}
@@ -70,6 +71,11 @@ for step in "$@"; do
     phases)
       timeout -k 10 600 python -u tools/phase_profile.py sail_amd/lib/libsail_hip_phase.so ${PHASE_SCENES:-C1 C3 C4} > $OUT/phases.jsonl 2>&1 || { tail $OUT/phases.jsonl; exit 11; }
       cat $OUT/phases.jsonl ;;
+    torchrun)  # bench.py under torch.distributed.run at N = 1 (the launcher the driver uses for N > 1)
+      timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_torchrun.log \
+        2> $OUT/bench_torchrun.err || { tail $OUT/bench_torchrun.err; exit 13; }
+      cut -c1-300 $OUT/bench_torchrun.log ;;
     jshost)
       timeout -k 10 300 node sail_amd/js/tools/bench_host.js > $OUT/bench_js_host.json 2> $OUT/bench_js_host.err || exit 12
       cut -c1-300 $OUT/bench_js_host.json ;;
