@@ -45,6 +45,8 @@ for step in "$@"; do
       vb unroll_C4 500 C4 base=main unroll=$V/libsail_hip_cull_unroll.so ;;
     cull_unroll8) # eight rows per step instead of four (study build cull_unroll8)
       vb unroll8_C4 500 C4 base=main unroll8=$V/libsail_hip_cull_unroll8.so ;;
+    cull_ldsfit) # LDS scene tables unconditional: ds_read instead of flat loads (study build cull_ldsfit; C4 fits)
+      vb ldsfit_C4 500 C4 base=main ldsfit=$V/libsail_hip_cull_ldsfit.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
