@@ -276,6 +276,7 @@ bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* 
   spec.ks = p.shape_mask; spec.km = p.material_mask; spec.kt = p.texture_mask; spec.kl = p.light_mask;
   spec.mode = m;
   spec.waves = jitWaves(m, set);
+  spec.ldsFit = (m == SAIL_JIT_MODE_CULL && c->n <= SAIL_CULL_LDS_ROWS && c->tn <= SAIL_CULL_LDS_TP) ? 1 : 0;
   if (rows && m != SAIL_JIT_MODE_CULL) {
     spec.rows = c->n;
     for (int i = 0; i < c->n; i++) spec.types[i] = c->primTypes[i];

@@ -104,6 +104,9 @@ enum { SAIL_KSET_GENERIC = 0, SAIL_KSET_CORNELL = 1, SAIL_KSET_ROOM = 2 };
 #define SAIL_GROUP_HOME_FOR(kernelSet) ((kernelSet) == SAIL_KSET_ROOM)
 // the exact segment counter is kept as this many partial sums (spread atomics), added on readback
 #define SAIL_SEG_SLOTS 64
+// the pre-cull kernels' per-workgroup LDS copies of the scene tables (rows of SailPrim, texParams rows of 16 floats)
+#define SAIL_CULL_LDS_ROWS 72
+#define SAIL_CULL_LDS_TP 136
 #define SAIL_KSET_CORNELL_SHAPES ((1u << SAIL_CUBE) | (1u << SAIL_SPHERE) | (1u << SAIL_CORNELLBOX))
 #define SAIL_KSET_CORNELL_MATS ((1u << SAIL_MATTE) | (1u << SAIL_MIRROR))
 #define SAIL_KSET_CORNELL_TEX 0u

@@ -10,6 +10,7 @@ struct SailJitSpec {
   int mode = 0;                             // sail_jit_mode (include/sail_hip.h): 0 flat, 1 pre-cull, 2 room family
   int waves = 6;                            // launch bounds: waves per SIMD
   int rows = 0;                             // > 0: the scene's row count, with each row's shape id in types
+  int ldsFit = 0;                           // pre-cull: the scene's tables fit the LDS copies (SAIL_CULL_LDS_*)
   int types[kSailJitMaxRows] = {};
 };
 // the kernel pair for `spec` on `device` (the current device), compiled and loaded on first use

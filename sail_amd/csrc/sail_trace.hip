@@ -1683,7 +1683,16 @@ D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
 // VGPRs); in the room kernel C3 -25 % (its spills 41 -> 85).
 // NT threads per workgroup: a 16 x NT/16 pixel block, 4096/NT blocks per 64x64 tile. A larger workgroup sorts a
 // larger pool of paths (fewer mixed waves) at the price of a wider barrier.
-constexpr int kCullLdsRows = 72, kCullLdsTp = 136;
+constexpr int kCullLdsRows = SAIL_CULL_LDS_ROWS, kCullLdsTp = SAIL_CULL_LDS_TP;
+// A pre-cull kernel compiled at run time for a scene whose tables fit (SAIL_JIT_LDSFIT) copies them unconditionally:
+// the per-lane row and texParams pointers are then known to point into LDS, so those reads are ds_read instead of flat
+// loads, which also wait on every outstanding vector-memory load, scratch reloads included (C4 +3.1 %,
+// profiles/r04_cull_ldsfit.jsonl).
+#if defined(SAIL_JIT) && SAIL_JIT_LDSFIT
+constexpr bool kLdsFitAll = true;
+#else
+constexpr bool kLdsFitAll = false;
+#endif
 constexpr int kPrioMixed = 2;
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
@@ -1748,8 +1757,11 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr int kLdsRows = CULL ? kCullLdsRows : 0;
   c.rowCopy = CULL;
   __shared__ float4 sPrimL[kLdsRows > 0 ? kLdsRows * (int)(sizeof(SailPrim) / 16) : 1];
+  if constexpr (kLdsFitAll) {
+    if (A.n > kLdsRows || A.tn > kCullLdsTp) return;  // never launched so (sail_capi.cpp jitKernels); uniform
+  }
   if constexpr (kLdsRows > 0) {
-    if (A.n <= kLdsRows) {  // uniform
+    if (kLdsFitAll || A.n <= kLdsRows) {  // uniform
       const float4* src = reinterpret_cast<const float4*>(A.prims);
       const int nv = A.n * (int)(sizeof(SailPrim) / 16);
       for (int i = li; i < nv; i += NT) sPrimL[i] = src[i];
@@ -1760,7 +1772,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   c.tpCopy = kLdsTp > 0;
   __shared__ float4 sTpL[kLdsTp > 0 ? kLdsTp * 4 : 1];
   if constexpr (kLdsTp > 0) {
-    if (A.tn <= kLdsTp) {  // uniform
+    if (kLdsFitAll || A.tn <= kLdsTp) {  // uniform
       const float4* src = reinterpret_cast<const float4*>(A.texparams);
       for (int i = li; i < A.tn * 4; i += NT) sTpL[i] = src[i];
       c.tpl = reinterpret_cast<const float*>(sTpL);
