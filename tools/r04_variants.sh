@@ -47,6 +47,8 @@ for step in "$@"; do
       vb unroll8_C4 500 C4 base=main unroll8=$V/libsail_hip_cull_unroll8.so ;;
     cull_ldsfit) # LDS scene tables unconditional: ds_read instead of flat loads (study build cull_ldsfit; C4 fits)
       vb ldsfit_C4 500 C4 base=main ldsfit=$V/libsail_hip_cull_ldsfit.so ;;
+    flat_lds)    # typed LDS scene tables in the flat kernels (study build flat_lds; C1, C3, UI fit)
+      for sc in C1 C3 UI; do vb flatlds_$sc 400 $sc base=main flatlds=$V/libsail_hip_flat_lds.so; done ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
