@@ -1693,6 +1693,16 @@ constexpr bool kLdsFitAll = true;
 #else
 constexpr bool kLdsFitAll = false;
 #endif
+// A flat kernel compiled for the scene's rows (kRows > 0) and its texParams row count (SAIL_JIT_TN > 0, at most 32 so
+// that the Cornell form keeps 8 workgroups per CU) copies both tables into LDS the same way: the per-lane row reads of
+// mixed waves' hit records and the material / texture reads become ds_read, off the counter the scratch reloads wait
+// on (C3 +2.8 %, UI +2.2 %, profiles/r04_flat_lds.jsonl; the host asks for it in the room form only: the Cornell form
+// measured -0.5 %). Round 3's flat-kernel copies were conditional (flat loads) and lost.
+#if defined(SAIL_JIT) && defined(SAIL_JIT_TN) && SAIL_JIT_TN > 0
+constexpr int kFlatTp = SAIL_JIT_TN;
+#else
+constexpr int kFlatTp = 0;
+#endif
 constexpr int kPrioMixed = 2;
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
@@ -1754,25 +1764,29 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   if (li < 2) sShCnt[li] = 0;
   // the pre-cull kernel's candidate loops, hit record and light sampler read rows per lane: from an LDS copy of the
   // scene when it fits
-  constexpr int kLdsRows = CULL ? kCullLdsRows : 0;
-  c.rowCopy = CULL;
+  constexpr int kLdsRows = CULL ? kCullLdsRows : (!CULL && kFlatTp > 0 && kRows > 0 ? kRows : 0);
+  c.rowCopy = kLdsRows > 0;
   __shared__ float4 sPrimL[kLdsRows > 0 ? kLdsRows * (int)(sizeof(SailPrim) / 16) : 1];
+  constexpr bool kFlatLds = !CULL && kFlatTp > 0 && kRows > 0;
   if constexpr (kLdsFitAll) {
     if (A.n > kLdsRows || A.tn > kCullLdsTp) return;  // never launched so (sail_capi.cpp jitKernels); uniform
   }
+  if constexpr (kFlatLds) {
+    if (A.n != kRows || A.tn != kFlatTp) return;  // never launched so (sail_capi.cpp jitKernels); uniform
+  }
   if constexpr (kLdsRows > 0) {
-    if (kLdsFitAll || A.n <= kLdsRows) {  // uniform
+    if (kLdsFitAll || kFlatLds || A.n <= kLdsRows) {  // uniform
       const float4* src = reinterpret_cast<const float4*>(A.prims);
       const int nv = A.n * (int)(sizeof(SailPrim) / 16);
       for (int i = li; i < nv; i += NT) sPrimL[i] = src[i];
       c.cprims = reinterpret_cast<const SailPrim*>(sPrimL);
     }
   }
-  constexpr int kLdsTp = CULL ? kCullLdsTp : 0;
+  constexpr int kLdsTp = CULL ? kCullLdsTp : (!CULL && kFlatTp > 0 && kRows > 0 ? kFlatTp : 0);
   c.tpCopy = kLdsTp > 0;
   __shared__ float4 sTpL[kLdsTp > 0 ? kLdsTp * 4 : 1];
   if constexpr (kLdsTp > 0) {
-    if (kLdsFitAll || A.tn <= kLdsTp) {  // uniform
+    if (kLdsFitAll || kFlatLds || A.tn <= kLdsTp) {  // uniform
       const float4* src = reinterpret_cast<const float4*>(A.texparams);
       for (int i = li; i < A.tn * 4; i += NT) sTpL[i] = src[i];
       c.tpl = reinterpret_cast<const float*>(sTpL);
