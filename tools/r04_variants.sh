@@ -49,6 +49,8 @@ for step in "$@"; do
       vb ldsfit_C4 500 C4 base=main ldsfit=$V/libsail_hip_cull_ldsfit.so ;;
     flat_lds)    # typed LDS scene tables in the flat kernels (study build flat_lds; C1, C3, UI fit)
       for sc in C1 C3 UI; do vb flatlds_$sc 400 $sc base=main flatlds=$V/libsail_hip_flat_lds.so; done ;;
+    cornell_tp)  # the Cornell form with only texParams in LDS (study build cornell_tp_lds)
+      vb cornelltp_C1 400 C1 base=main tplds=$V/libsail_hip_cornell_tp_lds.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
