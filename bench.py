@@ -146,16 +146,19 @@ def ops_per_segment(sc, masks, mvp, W, H, B):
     return ops / max(segs, 1), oracle.ops_live() / max(segs, 1)
 
 
-def profiled_traffic(workload, px, spp, bounces, kernel):
-    """HBM bytes per trace launch from the newest committed rocprofv3 PMC summary of the same workload, launch shape
-    and trace kernel (tools/pmc.sh + tools/pmc_summary.py -> profiles/r*_pmc_summary*.json); None if none matches."""
+def profiled_traffic(workload, px, spp, bounces, kernel_id):
+    """HBM bytes per trace launch from the committed rocprofv3 PMC summary (tools/pmc.sh + tools/pmc_summary.py ->
+    profiles/r*_pmc_summary*.json) of the same workload, launch shape and kernel BUILD: the summary records the
+    kernel_id ("name@build id": FNV-1a 64 of the run-time kernel's code object, or of the library image for a
+    precompiled kernel) its profiled bench printed, and only an equal id matches. None when no summary profiled this
+    very kernel (a rebuilt kernel is never matched to an older one's counters)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
         L = rec.get("launch", {})
-        if (rec.get("workload", "cornell_box_readme_C2") == workload and L.get("pixels") == px and L.get("spp") == spp
-                and L.get("bounces") == bounces and rec.get("kernel") == kernel):
+        if (rec.get("workload") == workload and L.get("pixels") == px and L.get("spp") == spp
+                and L.get("bounces") == bounces and kernel_id and rec.get("kernel_id") == kernel_id):
             return rec["hbm"]["traffic_bytes"], os.path.relpath(path, ROOT), rec
     return None, None, None
 
@@ -307,6 +310,9 @@ def main():
         ctx.set_debug(opt, val)
     ctx.set_scene_dict(sc)
     ctx.set_launch_samples(args.launch_spp)
+    # the scene's run-time kernel (built in the background at set_scene; from the cache shipped beside the library for
+    # the frozen scenes) before the warm-up, so every timed launch runs it
+    ctx.kernel_ready(-1)
     part = capi.PART_SAMPLES if cfg.get("partition") == "samples" else capi.PART_TILES
     flt = sc.get("filter") if cfg.get("filter") else None
     fweights = np.array(flt["weights64"], dtype=np.float32) if flt else None
@@ -374,7 +380,9 @@ def main():
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         achieved_live = ops_live * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
-        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B, ctx.kernel_name())
+        kinfo = ctx.kernel_info()
+        kernel_id = f"{kinfo['name']}@{kinfo['build_id']}"
+        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B, kernel_id)
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
@@ -408,6 +416,10 @@ def main():
                 "ops_per_segment_full": round(ops_seg, 2), "achieved_full": round(achieved_tflops, 3),
                 "frac_full": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
                 "kernel": ctx.kernel_name(),
+                "kernel_id": kernel_id,
+                "jit": {"state": ["none", "pending", "ready", "failed"][kinfo["jit_state"]],
+                        "code_object_from": ["hipRTC in this process", "user disk cache", "cache shipped with the library"][kinfo["jit_from_cache"]],
+                        "compile_ms": round(kinfo["jit_compile_ms"], 1), **({"error": kinfo["jit_error"]} if kinfo["jit_error"] else {})},
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 # one launch = the HIP events around the trace kernel and, with sample groups (a "_grouped" kernel),
                 # the sail_accum_kernel that adds the staged samples in order after it

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SAIL_ABI_VERSION 3
+#define SAIL_ABI_VERSION 4
 
 enum sail_status {
   SAIL_OK = 0,
@@ -123,7 +123,11 @@ enum sail_debug_option {
    * room-family kernel (SAIL_JIT_MODE_ROOM) instead of a plain one, 4 scenes of the room kernel's set, 2 pre-cull-path
    * scenes, 16 every flat-path scene of at most 8 primitives compiled for its rows too (their count and shape types).
    * 0: the precompiled kernels only. Same results [27 = 1 + 2 + 8 + 16; measured in profiles/r04_jit_*.jsonl] */
-  SAIL_DEBUG_JIT = 9
+  SAIL_DEBUG_JIT = 9,
+  /* how long (ms) a launch waits for the scene's run-time kernel while it is still being built in the background; -1:
+   * until it is built. Meanwhile the precompiled kernel of the scene's set renders, with the same results [0: never
+   * wait, so Renderer.update / render stay interactive; the Python binding used by the tests and bench.py sets -1] */
+  SAIL_DEBUG_JIT_WAIT = 10
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 
@@ -191,6 +195,42 @@ enum sail_jit_mode {
  * (SAIL_CUBE ..., each in plugins->shape_mask): the primitive sweeps become straight-line code over the rows */
 int sail_jit_compile(const sail_plugins* plugins, int mode, const int32_t* row_types, int rows, void* code,
                      size_t* bytes);
+/* The reference links a scene's program inside Renderer.update in milliseconds (src/core/renderer.js:45-52 ->
+ * tracer.js:42-90 -> webgl.js:165-192); a hipRTC compile takes seconds, so sail_set_scene / sail_update_objects only
+ * START the build of the scene's run-time kernel, on a background thread, and return; launches use the precompiled
+ * kernel of the scene's plugin set until the module is loaded (bit-identical frames). Code objects are cached on disk,
+ * keyed by (arch, spec, kernel-source hash, compile flags, hipRTC version): a read-only cache beside the library
+ * (<lib dir>/jit, filled by sail_jit_prebuild at build time) and the user's cache. A hipRTC whose version differs from
+ * the library's build is refused (the precompiled kernels serve). */
+enum sail_kernel_jit_state {
+  SAIL_KERNEL_JIT_NONE = 0,     /* the scene gets no run-time kernel (switches, or a precompiled kernel is exact) */
+  SAIL_KERNEL_JIT_PENDING = 1,  /* being built in the background */
+  SAIL_KERNEL_JIT_READY = 2,    /* loaded: launches use it */
+  SAIL_KERNEL_JIT_FAILED = 3    /* could not be built or loaded (jit_error): the precompiled kernel serves */
+};
+typedef struct sail_kernel_info {
+  char name[64];          /* the kernel the last launch ran (sail_kernel_name) */
+  uint64_t build_id;      /* its build identity: FNV-1a 64 of the code object (run-time kernels) or of the library
+                           * image and the kernel's name (precompiled): profiles are matched to kernels by it */
+  int jit_state;          /* sail_kernel_jit_state of the scene's run-time kernel */
+  int jit_from_cache;     /* its code object came from 0: hipRTC in this process, 1: the user's disk cache, 2: the
+                           * cache shipped beside the library */
+  double jit_compile_ms;  /* hipRTC time of that code object (0 from a cache) */
+  uint64_t jit_build_id;  /* the run-time kernel's build identity once READY */
+  char jit_error[256];    /* why it FAILED */
+} sail_kernel_info;
+int sail_get_kernel_info(sail_ctx* ctx, sail_kernel_info* out);
+/* *ready = 1 when the scene's run-time kernel is loaded (the next launch uses it), after waiting up to timeout_ms for
+ * its build (-1: until done); 0 while it is still building, when none applies, or when it failed */
+int sail_kernel_ready(sail_ctx* ctx, int timeout_ms, int* ready);
+/* process-wide user cache directory of run-time code objects: NULL = default ($XDG_CACHE_HOME or $HOME/.cache, then
+ * sail_amd/jit), "" = no user cache */
+int sail_set_jit_cache(const char* dir);
+/* Host only (no device): build the run-time kernel a context with the default switches derives for this scene (the rows
+ * of sail_set_scene) for `arch`, into the cache directory `dir` (the shipped cache when dir is <lib dir>/jit). *built
+ * (may be NULL) = 1 when the scene gets a run-time kernel, 0 when it does not. */
+int sail_jit_prebuild(const float* objects, int n, const float* texparams, int tn, const float* lights, int ln,
+                      const sail_plugins* plugins, const char* arch, const char* dir, int* built);
 
 /* ---- host math of the reference, so every host language gets identical uniforms ---- */
 /* Camera(eye, center, up) + makePerspective(fovy, aspect, near, far) (src/scene/camera.js:6-57):

@@ -28,6 +28,8 @@ DEBUG_WAVEFRONT = 6
 DEBUG_GROUP_ROUNDS = 7
 DEBUG_CULL_GROUP_ROUNDS = 8
 DEBUG_JIT = 9
+DEBUG_JIT_WAIT = 10  # ms a launch waits for the scene's run-time kernel (-1: until built; the C ABI's default is 0)
+KERNEL_JIT_NONE, KERNEL_JIT_PENDING, KERNEL_JIT_READY, KERNEL_JIT_FAILED = 0, 1, 2, 3
 JIT_MODE_FLAT, JIT_MODE_CULL, JIT_MODE_ROOM = 0, 1, 2  # sail_jit_compile kernel forms (include/sail_hip.h)
 # applied to every Context at creation (tests set entries with monkeypatch.setitem)
 DEBUG_DEFAULTS: dict = {}
@@ -41,6 +43,7 @@ EXPORTS = (
     "sail_comm_unique_id", "sail_comm_init", "sail_reduce", "sail_accum_device_ptr", "sail_partition_tiles",
     "sail_prim_bounds", "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
     "sail_abi_version", "sail_accum_parts", "sail_save_accum", "sail_load_accum", "sail_jit_compile",
+    "sail_get_kernel_info", "sail_kernel_ready", "sail_set_jit_cache", "sail_jit_prebuild",
 )
 
 
@@ -57,6 +60,12 @@ class Stats(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64),
                 ("nominal_segments", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("last_launch_ms", ctypes.c_double), ("launches", ctypes.c_uint32)]
+
+
+class KernelInfo(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 64), ("build_id", ctypes.c_uint64), ("jit_state", ctypes.c_int),
+                ("jit_from_cache", ctypes.c_int), ("jit_compile_ms", ctypes.c_double), ("jit_build_id", ctypes.c_uint64),
+                ("jit_error", ctypes.c_char * 256)]
 
 
 _SHAPES = {"cube": 1, "sphere": 2, "rectangle": 3, "cone": 4, "cylinder": 5, "disk": 6,
@@ -134,6 +143,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_load_accum": (ctypes.c_int, [vp, ctypes.c_int, f32p, ctypes.c_uint64]),
         "sail_jit_compile": (ctypes.c_int, [ctypes.POINTER(Plugins), ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                             vp, ctypes.POINTER(ctypes.c_size_t)]),
+        "sail_get_kernel_info": (ctypes.c_int, [vp, ctypes.POINTER(KernelInfo)]),
+        "sail_kernel_ready": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+        "sail_set_jit_cache": (ctypes.c_int, [ctypes.c_char_p]),
+        "sail_jit_prebuild": (ctypes.c_int, [f32p, ctypes.c_int, f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.POINTER(Plugins),
+                                             ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -240,6 +254,26 @@ def device_info(device: int = 0):
     return cus.value, khz.value * 1e3
 
 
+def set_jit_cache(path: Optional[str]):
+    """The process-wide user cache of run-time code objects (None: the default under ~/.cache, "": none)."""
+    load().sail_set_jit_cache(None if path is None else path.encode())
+
+
+def jit_prebuild(sc: dict, arch: str = "gfx950", cache_dir: Optional[str] = None) -> bool:
+    """Host-only: build the run-time kernel a default context derives for scene `sc` into `cache_dir` (default: the
+    cache shipped beside the library, sail_amd/lib/jit). Returns whether the scene gets one."""
+    lib = load()
+    o, t, l = _f32(sc["objects"]), _f32(sc["texparams"]), _f32(sc["lights"])
+    pl = Plugins(*[int(m) for m in plugin_masks(sc["plugins"])])
+    built = ctypes.c_int(0)
+    d = cache_dir or os.path.join(_HERE, "lib", "jit")
+    rc = lib.sail_jit_prebuild(_ptr(o), sc["n"], _ptr(t), sc["tn"], _ptr(l), sc["ln"], ctypes.byref(pl), arch.encode(),
+                               d.encode(), ctypes.byref(built))
+    if rc:
+        raise SailError(f"sail_jit_prebuild: {rc}: {lib.sail_last_error(None).decode()}")
+    return bool(built.value)
+
+
 def comm_unique_id() -> bytes:
     lib = load()
     buf = ctypes.create_string_buffer(128)
@@ -271,7 +305,9 @@ class Context:
         self.h = h
         self._accum_mode = ACCUM_SUM          # the C ABI's default (sail_create)
         self._partition = (0, 1, PART_TILES)  # (rank, world, mode): checkpoints record and check these
-        for opt, val in {**DEBUG_DEFAULTS, **(debug or {})}.items():
+        # the tests and bench.py want the scene's run-time kernel from the first launch (the C ABI's interactive default,
+        # 0, launches the precompiled kernel until the background build is done; tests set 0 to render across the swap)
+        for opt, val in {DEBUG_JIT_WAIT: -1, **DEBUG_DEFAULTS, **(debug or {})}.items():
             self.set_debug(opt, val)
 
     def set_debug(self, option: int, value: int):
@@ -368,6 +404,23 @@ class Context:
         buf = ctypes.create_string_buffer(64)
         self._check(self.lib.sail_kernel_name(self.h, buf, 64), "sail_kernel_name")
         return buf.value.decode()
+
+    def kernel_info(self) -> dict:
+        k = KernelInfo()
+        self._check(self.lib.sail_get_kernel_info(self.h, ctypes.byref(k)), "sail_get_kernel_info")
+        return {"name": k.name.decode(), "build_id": f"{k.build_id:016x}", "jit_state": k.jit_state,
+                "jit_from_cache": k.jit_from_cache, "jit_compile_ms": k.jit_compile_ms,
+                "jit_build_id": f"{k.jit_build_id:016x}", "jit_error": k.jit_error.decode()}
+
+    def kernel_id(self) -> str:
+        """the last launch's kernel and its build identity, "name@hex16" (profiles are matched to kernels by it)"""
+        k = self.kernel_info()
+        return f"{k['name']}@{k['build_id']}"
+
+    def kernel_ready(self, timeout_ms: int = -1) -> bool:
+        r = ctypes.c_int(0)
+        self._check(self.lib.sail_kernel_ready(self.h, int(timeout_ms), ctypes.byref(r)), "sail_kernel_ready")
+        return bool(r.value)
 
     def stats(self) -> Stats:
         s = Stats()

@@ -146,10 +146,19 @@ struct sail_ctx {
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
   int jit = sail_trace_phase_timing ? 0 : 27;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels)
-  bool jitFailed = false;  // hipRTC or the module load failed once: the all-plugin kernel serves this context
-  std::string jitError;
+  // The scene's run-time kernel (refreshJit): its spec, and whether it is still being built, loaded or failed. Until it
+  // is loaded the precompiled kernel of the scene's set serves (same results); a launch waits up to jitWait ms for it
+  // (SAIL_DEBUG_JIT_WAIT; -1 until it is built).
+  bool jitHave = false;
+  SailJitSpec jitSpec;
+  int jitMode = 0;
+  int jitState = SAIL_KERNEL_JIT_NONE;
+  SailJitKernel jitK;
+  std::string jitError;  // why the scene's run-time kernel failed (sail_get_kernel_info)
+  int jitWait = 0;
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
   int lastJitMode = 0;
+  uint64_t lastBuildId = 0;  // the run-time kernel's build identity (sail_get_kernel_info)
   std::vector<int> primTypes;  // decoded shape id of each row (run-time kernels compiled for the scene's rows)
   float4* wf = nullptr;  // its path state: 11 float4 arrays of wfSlots
   size_t wfSlots = 0;
@@ -225,9 +234,6 @@ int loadIncomplete(sail_ctx* c, const char* what) {
   } while (0)
 
 // the smallest precompiled plugin-set kernel that covers the scene (sail_device.h SAIL_KSET_*)
-// The run-time compiled kernel of the scene's plugin set (sail_jit.cpp); false when it does not apply or could not be
-// built (the precompiled kernel of the scene's set then runs, with the same results). *mode: SAIL_JIT_MODE_*.
-bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* mode);
 int kernelSetFor(const sail_ctx* c) {
   if (c->forceGeneric || c->n >= c->cullMinPrims) return SAIL_KSET_GENERIC;
   const sail_plugins& p = c->plugins;
@@ -250,10 +256,11 @@ int jitWaves(int mode, int kernelSet) {
   if (mode == SAIL_JIT_MODE_ROOM) return kernelSet == SAIL_KSET_ROOM ? 7 : 8;
   return kernelSet == SAIL_KSET_CORNELL ? 8 : 6;
 }
+// The run-time kernel spec of the context's scene under its switches, or false when none applies.
 // SAIL_DEBUG_JIT bits (include/sail_hip.h): 1 flat scenes outside the Cornell and room sets, 2 pre-cull scenes, 4 room-set
 // scenes, 8 the flat scenes of bit 1 in the room form, 16 flat scenes compiled for their rows as well (any flat scene).
-bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* mode) {
-  if (!c->jit || c->jitFailed || !c->haveScene || c->forceGeneric) return false;
+bool jitSpecFor(const sail_ctx* c, SailJitSpec* out, int* mode) {
+  if (!c->jit || !c->haveScene || c->forceGeneric) return false;
   const int set = kernelSetFor(c);
   const bool rows = (c->jit & 16) && c->n >= 1 && c->n <= kSailJitMaxRows && c->n < c->cullMinPrims &&
                     (int)c->primTypes.size() == c->n;
@@ -286,13 +293,43 @@ bool jitKernels(sail_ctx* c, hipFunction_t* plain, hipFunction_t* grouped, int* 
     // the room form copies both tables into LDS (C3 +2.8 %, UI +2.2 %; the Cornell form measured -0.5 %)
     if (spec.rows && m == SAIL_JIT_MODE_ROOM && c->tn >= 1 && c->tn <= kSailJitMaxFlatTp) spec.tn = c->tn;
   }
-  std::string err;
-  if (sail_jit_kernels(c->device, spec, plain, grouped, &err)) {
-    c->jitFailed = true;
-    c->jitError = err;
-    return false;
-  }
+  *out = spec;
   *mode = m;
+  return true;
+}
+// Re-derive the scene's run-time kernel after anything it depends on changed (scene, rows, switches). A new spec starts
+// its background build now (Tracer.update links the scene's program, tracer.js:42-90), so the caller never waits for it.
+void refreshJit(sail_ctx* c) {
+  SailJitSpec spec;
+  int mode = 0;
+  const bool have = jitSpecFor(c, &spec, &mode);
+  if (have == c->jitHave && (!have || sailJitSpecEqual(spec, c->jitSpec))) return;
+  c->jitHave = have;
+  c->jitSpec = spec;
+  c->jitMode = mode;
+  c->jitK = SailJitKernel{};
+  c->jitError.clear();
+  c->jitState = have ? SAIL_KERNEL_JIT_PENDING : SAIL_KERNEL_JIT_NONE;
+  if (!have) return;
+  std::string err;
+  const int r = sail_jit_kernels(c->device, spec, 0, &c->jitK, &err);  // starts the build; loads it if it is cached
+  if (r == 0) c->jitState = SAIL_KERNEL_JIT_READY;
+  else if (r < 0) { c->jitState = SAIL_KERNEL_JIT_FAILED; c->jitError = err; }
+}
+// The run-time compiled kernel of the scene's plugin set (sail_jit.cpp), waiting up to wait_ms for its build; false when
+// none applies, it is still being built or it failed (the precompiled kernel of the scene's set then runs, with the same
+// results). *mode: SAIL_JIT_MODE_*.
+bool jitKernels(sail_ctx* c, int wait_ms, SailJitKernel* k, int* mode) {
+  if (!c->jitHave || c->jitState == SAIL_KERNEL_JIT_FAILED) return false;
+  if (c->jitState != SAIL_KERNEL_JIT_READY) {
+    std::string err;
+    const int r = sail_jit_kernels(c->device, c->jitSpec, wait_ms, &c->jitK, &err);
+    if (r == 1) return false;
+    if (r < 0) { c->jitState = SAIL_KERNEL_JIT_FAILED; c->jitError = err; return false; }
+    c->jitState = SAIL_KERNEL_JIT_READY;
+  }
+  *k = c->jitK;
+  *mode = c->jitMode;
   return true;
 }
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
@@ -724,9 +761,9 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
     const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
-    hipFunction_t jp = nullptr, jg = nullptr;
+    SailJitKernel jk;
     int jmode = 0;
-    const bool jit = !wavefront && jitKernels(c, &jp, &jg, &jmode);
+    const bool jit = !wavefront && jitKernels(c, c->jitWait, &jk, &jmode);
     A.groupHome = (jit ? jmode == SAIL_JIT_MODE_ROOM : SAIL_GROUP_HOME_FOR(A.kernelSet)) ? 1 : 0;
     A.stageStride = stageStride;
     const bool staged = A.sampleGroups > 1;
@@ -764,10 +801,11 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       if (jit) {
         void* args[] = {&A};
         const unsigned nt = jmode == SAIL_JIT_MODE_CULL ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips
-        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jg : jp, (unsigned)(owned * 16 * A.sampleGroups) * 256u / nt, 1,
+        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jk.grouped : jk.plain, (unsigned)(owned * 16 * A.sampleGroups) * 256u / nt, 1,
                                         1, nt, 1, 1, 0, c->stream, args, nullptr));
         c->lastJit = true;
         c->lastJitMode = jmode;
+        c->lastBuildId = jk.buildId;
       } else {
         HIPCHK(c, sail_launch_trace(A, owned * 16 * A.sampleGroups, c->stream));
         c->lastJit = false;
@@ -946,6 +984,50 @@ int sail_kernel_name(sail_ctx* c, char* name, int len) {
   return SAIL_OK;
 }
 
+int sail_get_kernel_info(sail_ctx* c, sail_kernel_info* out) {
+  if (!c || !out) return SAIL_E_INVALID;
+  if (!c->subs.empty()) return relay(c, sail_get_kernel_info(c->subs[0], out), c->subs[0]);
+  memset(out, 0, sizeof *out);
+  if (int rc = sail_kernel_name(c, out->name, (int)sizeof out->name)) return rc;
+  out->build_id = c->lastJit ? c->lastBuildId : sail_precompiled_build_id(out->name);
+  if (c->jitState == SAIL_KERNEL_JIT_PENDING) {  // poll the background build (loads the module when it is done)
+    SailJitKernel k;
+    int m;
+    (void)jitKernels(c, 0, &k, &m);
+  }
+  out->jit_state = c->jitState;
+  out->jit_build_id = c->jitState == SAIL_KERNEL_JIT_READY ? c->jitK.buildId : 0;
+  out->jit_compile_ms = c->jitK.compileMs;
+  out->jit_from_cache = c->jitK.fromCache;
+  snprintf(out->jit_error, sizeof out->jit_error, "%s", c->jitError.c_str());
+  return SAIL_OK;
+}
+
+int sail_kernel_ready(sail_ctx* c, int timeout_ms, int* ready) {
+  if (!c || !ready || timeout_ms < -1) return SAIL_E_INVALID;
+  *ready = 0;
+  if (!c->subs.empty()) {
+    int all = 1;
+    for (sail_ctx* s : c->subs) {
+      int r = 0;
+      if (int rc = sail_kernel_ready(s, timeout_ms, &r)) return relay(c, rc, s);
+      all &= r;
+    }
+    *ready = all;
+    return SAIL_OK;
+  }
+  if (!c->haveScene) return fail(c, SAIL_E_STATE, "sail_kernel_ready: no scene");
+  SailJitKernel k;
+  int m;
+  *ready = jitKernels(c, timeout_ms, &k, &m) ? 1 : 0;
+  return SAIL_OK;
+}
+
+int sail_set_jit_cache(const char* dir) {
+  sail_jit_set_cache_dir(dir);
+  return SAIL_OK;
+}
+
 int sail_device_count(int* count) {
   if (!count) return SAIL_E_INVALID;
   int n = 0;
@@ -1102,6 +1184,10 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
     case SAIL_DEBUG_JIT: c->jit = value; break;
+    case SAIL_DEBUG_JIT_WAIT:
+      if (value < -1) return fail(c, SAIL_E_INVALID, "sail_set_debug: jit wait must be >= -1");
+      c->jitWait = value;
+      break;
     case SAIL_DEBUG_GROUP_ROUNDS:
       if (value <= 0) return fail(c, SAIL_E_INVALID, "sail_set_debug: group rounds must be > 0");
       c->flatGroupRounds = value;
@@ -1112,6 +1198,7 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
       break;
     default: return fail(c, SAIL_E_INVALID, "sail_set_debug: unknown option %d", option);
   }
+  refreshJit(c);  // the switches decide which run-time kernel (if any) the scene gets
   return SAIL_OK;
 }
 
@@ -1141,6 +1228,7 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
     for (sail_ctx* s : c->subs)
       if (int rc = sail_set_scene(s, objects, n, texparams, tn, lights, ln, plugins)) return relay(c, rc, s);
     c->haveScene = true; c->n = n; c->tn = tn; c->ln = ln; c->dirty = false;
+    c->loadMissing = 0;  // every device's accumulation restarted: a half-loaded checkpoint is abandoned
     return SAIL_OK;
   }
   if (n < 0 || tn < 0 || ln < 0 || (n > 0 && !objects) || (tn > 0 && !texparams) || (ln > 0 && !lights) || !plugins)
@@ -1185,11 +1273,9 @@ int sail_set_scene(sail_ctx* c, const float* objects, int n, const float* texpar
   c->tpRows.assign(texparams, texparams + (size_t)tn * 16);
   c->n = n; c->tn = tn; c->ln = ln;
   c->haveScene = true;
-  {  // Tracer.update links the scene's program (tracer.js:42-90): compile the plugin set's kernel now, not at render
-    hipFunction_t jp, jg;
-    int jm;
-    (void)jitKernels(c, &jp, &jg, &jm);
-  }
+  // Tracer.update links the scene's program (tracer.js:42-90): the plugin set's kernel starts building now, in the
+  // background; the precompiled kernel of the set serves until it is loaded
+  refreshJit(c);
   return resetAccum(c);
 }
 
@@ -1197,6 +1283,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   if (c && !c->subs.empty()) {
     for (sail_ctx* s : c->subs) if (int rc = sail_update_objects(s, objects, n)) return relay(c, rc, s);
     c->dirty = false;
+    c->loadMissing = 0;
     return SAIL_OK;
   }
   if (!c || !c->haveScene) return c ? fail(c, SAIL_E_STATE, "sail_update_objects before sail_set_scene") : SAIL_E_INVALID;
@@ -1212,6 +1299,7 @@ int sail_update_objects(sail_ctx* c, const float* objects, int n) {
   if (int rc = uploadPrims(c, prims)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->objectsRows.assign(objects, objects + (size_t)n * 18);
+  refreshJit(c);  // a drag keeps the kernel; a changed shape type starts the new rows' kernel building
   return resetAccum(c);
 }
 
@@ -1221,6 +1309,7 @@ int sail_set_accum_mode(sail_ctx* c, int mode) {
   if (!c->subs.empty()) {
     for (sail_ctx* s : c->subs) if (int rc = sail_set_accum_mode(s, mode)) return relay(c, rc, s);
     c->accumMode = mode; c->dirty = false;
+    c->loadMissing = 0;
     return SAIL_OK;
   }
   if (mode != SAIL_ACCUM_SUM && c->partMode == SAIL_PART_SAMPLES && c->world > 1)
@@ -1238,6 +1327,7 @@ int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
     const int nd = (int)c->subs.size();
     for (int i = 0; i < nd; i++) if (int rc = sail_set_partition(c->subs[i], i, nd, mode)) return relay(c, rc, c->subs[i]);
     c->partMode = mode; c->dirty = false;
+    c->loadMissing = 0;
     return SAIL_OK;
   }
   if (world < 1 || rank < 0 || rank >= world || (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
@@ -1674,6 +1764,31 @@ int sail_jit_compile(const sail_plugins* plugins, int mode, const int32_t* row_t
   std::string err;
   if (sail_jit_code("gfx950", spec, code, bytes, &err))
     return fail(nullptr, SAIL_E_INVALID, "sail_jit_compile: %s", err.c_str());
+  return SAIL_OK;
+}
+
+int sail_jit_prebuild(const float* objects, int n, const float* texparams, int tn, const float* lights, int ln,
+                      const sail_plugins* plugins, const char* arch, const char* dir, int* built) {
+  if (n < 0 || tn < 0 || ln < 0 || (n > 0 && !objects) || (tn > 0 && !texparams) || (ln > 0 && !lights) || !plugins ||
+      !arch || (n > 0 && tn < 1))
+    return fail(nullptr, SAIL_E_INVALID, "sail_jit_prebuild: bad arguments");
+  (void)lights;
+  // the spec a context with the product's defaults derives for this scene (jitSpecFor), without a device
+  sail_ctx t;
+  t.plugins = *plugins;
+  t.n = n; t.tn = tn; t.ln = ln;
+  t.haveScene = true;
+  std::vector<SailPrim> prims;
+  int anyHit = 0;
+  decodePrims(objects, n, tn, plugins->shape_mask, prims, &anyHit, nullptr);
+  for (const SailPrim& q : prims) t.primTypes.push_back(q.type);
+  SailJitSpec spec;
+  int mode = 0;
+  if (built) *built = 0;
+  if (!jitSpecFor(&t, &spec, &mode)) return SAIL_OK;  // the scene gets no run-time kernel
+  std::string err;
+  if (sail_jit_code_to_dir(arch, spec, dir, &err)) return fail(nullptr, SAIL_E_INVALID, "sail_jit_prebuild: %s", err.c_str());
+  if (built) *built = 1;
   return SAIL_OK;
 }
 

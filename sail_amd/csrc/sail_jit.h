@@ -15,7 +15,25 @@ struct SailJitSpec {
   int tn = 0;                               // flat forms with rows: the texParams row count (LDS copies), 0 = none
   int types[kSailJitMaxRows] = {};
 };
-// the kernel pair for `spec` on `device` (the current device), compiled and loaded on first use
-int sail_jit_kernels(int device, const SailJitSpec& spec, hipFunction_t* plain, hipFunction_t* grouped, std::string* err);
-// host only: the code object for `arch`, compiled by the same path (sail_jit_compile)
+bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b);
+
+// A loaded kernel pair and where its code object came from.
+struct SailJitKernel {
+  hipFunction_t plain = nullptr, grouped = nullptr;
+  uint64_t buildId = 0;     // FNV-1a 64 of the code object (the kernel's build identity)
+  double compileMs = 0.0;   // hipRTC time of the code object (0 when it came from a disk cache)
+  int fromCache = 0;        // 1: the user's on-disk cache, 2: the cache shipped next to the library
+};
+// The kernel pair for `spec` on `device` (made current). The code object is built on a background thread at the first
+// request (disk caches first, then hipRTC), outside every lock the launch path takes. Returns 0 with the loaded pair;
+// 1 while the code object is still being built and wait_ms allows no more waiting (wait_ms < 0: wait until it is done);
+// -1 with a message when it cannot be built or loaded (the caller then runs the precompiled kernel, same results).
+int sail_jit_kernels(int device, const SailJitSpec& spec, int wait_ms, SailJitKernel* out, std::string* err);
+// host only: the code object for `arch`, built by the same path (sail_jit_compile, sail_jit_prebuild); blocks
 int sail_jit_code(const char* arch, const SailJitSpec& spec, void* code, size_t* bytes, std::string* err);
+// the on-disk code-object cache directory: nullptr = the default ($XDG_CACHE_HOME or $HOME/.cache, /sail_amd/jit),
+// "" = none (sail_set_jit_cache); `dir` of sail_jit_code / prebuild when it is not null
+void sail_jit_set_cache_dir(const char* dir);
+int sail_jit_code_to_dir(const char* arch, const SailJitSpec& spec, const char* dir, std::string* err);
+// FNV-1a 64 of the library image plus a precompiled kernel's name: the build identity of a precompiled kernel
+uint64_t sail_precompiled_build_id(const char* kernel);

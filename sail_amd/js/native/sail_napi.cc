@@ -385,6 +385,46 @@ napi_value Stats(napi_env env, napi_callback_info info) {
   napi_set_named_property(env, out, "launches", num(env, s.launches));
   return out;
 }
+// (ctx, timeoutMs) -> whether the scene's run-time kernel is loaded (sail_kernel_ready; -1 waits for its build)
+napi_value KernelReady(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  if (!args(env, info, 2, a)) return nullptr;
+  Handle* h;
+  int ms = 0;
+  if (!getHandle(env, a[0], &h) || !getInt(env, a[1], &ms)) return nullptr;
+  int ready = 0;
+  const int rc = sail_kernel_ready(h->ctx, ms, &ready);
+  if (rc) return throwSail(env, "sail_kernel_ready", rc, h->ctx);
+  napi_value out;
+  NAPI_OK(napi_get_boolean(env, ready != 0, &out));
+  return out;
+}
+// (ctx) -> {name, buildId, jitState, jitFromCache, jitCompileMs, jitError} (sail_get_kernel_info)
+napi_value KernelInfo(napi_env env, napi_callback_info info) {
+  napi_value a[1];
+  if (!args(env, info, 1, a)) return nullptr;
+  Handle* h;
+  if (!getHandle(env, a[0], &h)) return nullptr;
+  sail_kernel_info k;
+  const int rc = sail_get_kernel_info(h->ctx, &k);
+  if (rc) return throwSail(env, "sail_get_kernel_info", rc, h->ctx);
+  char id[17];
+  snprintf(id, sizeof id, "%016llx", (unsigned long long)k.build_id);
+  napi_value out, v;
+  NAPI_OK(napi_create_object(env, &out));
+  NAPI_OK(napi_create_string_utf8(env, k.name, NAPI_AUTO_LENGTH, &v));
+  napi_set_named_property(env, out, "name", v);
+  NAPI_OK(napi_create_string_utf8(env, id, NAPI_AUTO_LENGTH, &v));
+  napi_set_named_property(env, out, "buildId", v);
+  static const char* const states[] = {"none", "pending", "ready", "failed"};
+  NAPI_OK(napi_create_string_utf8(env, states[k.jit_state & 3], NAPI_AUTO_LENGTH, &v));
+  napi_set_named_property(env, out, "jitState", v);
+  napi_set_named_property(env, out, "jitFromCache", num(env, k.jit_from_cache));
+  napi_set_named_property(env, out, "jitCompileMs", num(env, k.jit_compile_ms));
+  NAPI_OK(napi_create_string_utf8(env, k.jit_error, NAPI_AUTO_LENGTH, &v));
+  napi_set_named_property(env, out, "jitError", v);
+  return out;
+}
 bool getVec(napi_env env, napi_value v, double* out, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) {
     napi_value e;
@@ -499,6 +539,8 @@ napi_value Init(napi_env env, napi_value exports) {
       {"loadAccum", 0, LoadAccum, 0, 0, 0, napi_enumerable, 0},
       {"filter", 0, Filter, 0, 0, 0, napi_enumerable, 0},
       {"stats", 0, Stats, 0, 0, 0, napi_enumerable, 0},
+      {"kernelReady", 0, KernelReady, 0, 0, 0, napi_enumerable, 0},
+      {"kernelInfo", 0, KernelInfo, 0, 0, 0, napi_enumerable, 0},
       {"pick", 0, Pick, 0, 0, 0, napi_enumerable, 0},
       {"camera", 0, Camera, 0, 0, 0, napi_enumerable, 0},
       {"jitterInverse", 0, JitterInverse, 0, 0, 0, napi_enumerable, 0},

@@ -58,6 +58,10 @@ class Renderer {
       : this.lib.create(this.width, this.height, this.device, flags);
     if (opts.partition === 'samples') this.lib.setPartition(this.ctx, 0, 1, 1);
     this.lib.setAccumMode(this.ctx, ACCUM[this.accumulation]);
+    // update() links the scene's program in the background (a hipRTC build takes seconds, the reference's GL link
+    // milliseconds: renderer.js:45-52); until it is loaded render() uses the precompiled kernel of the scene's plugin
+    // set, with identical frames. waitKernel (ms, -1 = until built) makes each launch wait for it instead [0].
+    if (opts.waitKernel !== undefined) this.lib.setDebug(this.ctx, 10, opts.waitKernel);
     this.timeStart = Date.now();
     this.filter = filterConfig({ name: 'color', params: {} });
     this.pixels = null;
@@ -164,6 +168,9 @@ class Renderer {
   readAccum() { return this.lib.readAccum(this.ctx); }
   readAOV() { const r = this.lib.readback(this.ctx, true); return { normal: r.normal, position: r.position }; }
   stats() { return this.lib.stats(this.ctx); }
+  // whether the scene's run-time compiled kernel serves the next render (waiting up to timeoutMs for its build)
+  kernelReady(timeoutMs = -1) { return this.lib.kernelReady(this.ctx, timeoutMs); }
+  kernelInfo() { return this.lib.kernelInfo(this.ctx); }
   destroy() { if (this.ctx) { this.lib.destroy(this.ctx); this.ctx = null; } }
 }
 

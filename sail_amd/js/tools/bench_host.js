@@ -32,6 +32,7 @@ function run(o, perFrame) {
   const r = new Sail.Renderer({ width: o.width, height: o.height, maxBounces: o.bounces, deterministic: true,
     accumulation: 'sum', aov: false, display: false });
   r.update(scene);
+  r.kernelReady(-1);  // the scene's run-time kernel, built in the background, serves every timed frame
   // warm-up (module load, first launches), then a fresh frame
   if (perFrame) for (let i = 0; i < 4; i++) r.render(scene); else r.renderSamples(scene, 32);
   r.readPixels();

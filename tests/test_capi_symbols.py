@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert capi.load().sail_abi_version() == 3
+    assert capi.load().sail_abi_version() == 4
 
 
 def test_library_targets_gfx950(tmp_path):

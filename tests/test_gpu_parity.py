@@ -782,3 +782,99 @@ def test_jit_precull_kernel_bit_exact(gpu, fixtures):
         finally:
             ctx.close()
         assert bit_equal(got, want).all(), dbg
+
+
+# ---- the scene's kernel built in the background ------------------------------------------------
+def _reversed_c1(fixtures):
+    """C1 with its object rows in reverse order: a row specialisation no other test and no shipped cache entry has"""
+    sc = dict(fixtures["scenes"]["C1"])
+    rows = np.asarray(sc["objects"], np.float32).reshape(sc["n"], 18)[::-1].copy()
+    sc["objects"] = rows.reshape(-1).tolist()
+    return sc
+
+
+SWAP_CHILD = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+from sail_amd import capi
+capi.set_jit_cache(sys.argv[2])
+sc = json.loads(open(sys.argv[3]).read())
+ctx = capi.Context(40, 24, debug={capi.DEBUG_JIT_WAIT: 0})
+t0 = time.perf_counter()
+ctx.set_scene_dict(sc)
+dt = time.perf_counter() - t0
+print(json.dumps({"set_scene_ms": dt * 1e3, "info": ctx.kernel_info()}))
+ctx.close()
+"""
+
+
+def test_jit_swap_mid_frame_bit_exact(gpu, fixtures, tmp_path):
+    """sail_set_scene returns at once (the reference's Renderer.update links in milliseconds, renderer.js:45-52) while the
+    scene's kernel is built in the background; the first samples render on the precompiled Cornell kernel, the rest on
+    the run-time kernel once it is loaded, and the frame across the swap equals the oracle's bit for bit. Then a new
+    process with the now-warm disk cache loads the kernel inside sail_set_scene."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+    sc = _reversed_c1(fixtures)
+    W, H, spp, B = 40, 24, 4, 6
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
+    cache = str(tmp_path / "jit")
+    capi.set_jit_cache(cache)
+    try:
+        ctx = capi.Context(W, H, debug={capi.DEBUG_JIT_WAIT: 0})
+        try:
+            t0 = time.perf_counter()
+            ctx.set_scene_dict(sc)
+            cold_ms = (time.perf_counter() - t0) * 1e3
+            assert ctx.kernel_info()["jit_state"] == capi.KERNEL_JIT_PENDING
+            ctx.render_schedule(inv[:2], seeds[:2], sc["eye"], B)
+            first = ctx.kernel_name()
+            assert ctx.kernel_ready(-1)
+            ctx.render_schedule(inv[2:], seeds[2:], sc["eye"], B)
+            second = ctx.kernel_name()
+            info = ctx.kernel_info()
+            got = ctx.read_accum()
+        finally:
+            ctx.close()
+    finally:
+        capi.set_jit_cache(None)
+    assert first.startswith("sail_trace_kernel_cornell"), first
+    assert second.startswith("sail_trace_kernel_jit"), second
+    assert info["jit_state"] == capi.KERNEL_JIT_READY and info["jit_from_cache"] == 0 and info["jit_compile_ms"] > 0
+    assert bit_equal(got, want).all()
+    assert cold_ms < 200.0, cold_ms
+    assert len(os.listdir(cache)) == 1  # the code object went to the user cache
+    scp = tmp_path / "scene.json"
+    scp.write_text(json.dumps(sc))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", SWAP_CHILD, root, cache, str(scp)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    warm = json.loads(r.stdout.strip().splitlines()[-1])
+    assert warm["info"]["jit_state"] == capi.KERNEL_JIT_READY and warm["info"]["jit_from_cache"] == 1, warm
+    assert warm["info"]["jit_build_id"] == info["jit_build_id"], warm
+    assert warm["set_scene_ms"] < 100.0, warm
+
+
+def test_kernel_build_identity(gpu, fixtures):
+    """sail_get_kernel_info: a run-time kernel's build id is its code object's hash (equal for equal specs, different
+    for another spec), a precompiled kernel's is the library image's plus its name"""
+    W, H, B = 32, 16, 4
+    ids = {}
+    for name, dbg in (("C1", {}), ("C3", {}), ("C1", {capi.DEBUG_JIT: 0})):
+        sc = fixtures["scenes"][name]
+        inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, 2)
+        ctx = capi.Context(W, H, debug=dbg)
+        try:
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            k = ctx.kernel_info()
+            ids[(name, bool(dbg))] = (k["name"], k["build_id"], k["jit_build_id"])
+        finally:
+            ctx.close()
+    (n1, b1, j1), (n3, b3, _), (n0, b0, j0) = ids[("C1", False)], ids[("C3", False)], ids[("C1", True)]
+    assert n1.startswith("sail_trace_kernel_jit") and b1 == j1 and b1 != b3
+    assert n0.startswith("sail_trace_kernel_cornell") and b0 != b1 and j0 == "0" * 16

@@ -144,18 +144,110 @@ def test_bad_specialisations_refused(fixtures):
     assert lib.sail_jit_compile(ctypes.byref(pl), 0, (ctypes.c_int32 * 9)(*[1] * 9), 9, None, ctypes.byref(n)) != 0
 
 
+def _child_compile(env, cache="", masks=(0x206, 6, 0, 0), mode=0):
+    """sail_jit_compile in a child process (the library opens hipRTC once per process): (rc, message, code sha)"""
+    child = (
+        "import ctypes, hashlib, sys\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
+        "from sail_amd import capi\n"
+        f"capi.set_jit_cache({cache!r})\n"
+        f"lib = capi.load(); pl = capi.Plugins(*{tuple(masks)!r}); n = ctypes.c_size_t(0)\n"
+        f"rc = lib.sail_jit_compile(ctypes.byref(pl), {mode}, None, 0, None, ctypes.byref(n))\n"
+        "buf = ctypes.create_string_buffer(max(n.value, 1))\n"
+        f"rc = rc or lib.sail_jit_compile(ctypes.byref(pl), {mode}, None, 0, buf, ctypes.byref(n))\n"
+        "print(rc, hashlib.sha256(buf.raw).hexdigest() if rc == 0 else '-', lib.sail_last_error(None).decode())\n")
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, sha, msg = (r.stdout.strip().splitlines()[-1].split(" ", 2) + [""])[:3]
+    return int(rc), msg, sha
+
+
 def test_missing_hiprtc_is_an_error_not_a_crash(tmp_path):
     """SAIL_HIPRTC naming a missing library: sail_jit_compile fails with the dlmopen message (contexts then keep the
-    precompiled kernels, tests/test_gpu_jit_fallback.py); a child process, as the library opens hipRTC once"""
+    precompiled kernels, tests/test_gpu_jit_fallback.py); no disk cache, so the code object must be compiled"""
+    env = dict(os.environ, SAIL_HIPRTC=str(tmp_path / "missing" / "libhiprtc.so.7"))
+    rc, msg, _ = _child_compile(env)
+    assert rc != 0 and "dlmopen" in msg, msg
+
+
+def _torch_hiprtc():
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "libhiprtc.so")
+    return p if os.path.exists(p) else None
+
+
+def test_other_hiprtc_is_refused(tmp_path):
+    """A hipRTC of another ROCm (PyTorch's, ROCm 7.0, under the same soname) compiles, but its code object's producer
+    is not the compiler that built this library's kernels: refused, so contexts keep the
+    precompiled kernels rather than run a kernel whose arithmetic another code generator chose"""
+    other = _torch_hiprtc()
+    if other is None:
+        pytest.skip("no second hipRTC in this image")
+    env = dict(os.environ, SAIL_HIPRTC=other, AMD_COMGR_CACHE="0")
+    rc, msg, _ = _child_compile(env)
+    assert rc != 0 and "produced by clang" in msg, msg
+
+
+def test_disk_cache_round_trip_and_corruption(tmp_path):
+    """The code object lands in the user cache; a new process reads it back (same bytes); a corrupted file is
+    rejected by its checksum and rebuilt, and the rebuilt file is whole again"""
+    cache = str(tmp_path / "jit")
+    env = dict(os.environ, AMD_COMGR_CACHE="0")
+    masks = (0x206 | 8, 6, 0, 0)  # a set no other test compiles
+    rc, _, sha1 = _child_compile(env, cache, masks)
+    assert rc == 0
+    files = sorted(os.listdir(cache))
+    assert len(files) == 1 and files[0].endswith(".co")
+    path = os.path.join(cache, files[0])
+    raw = open(path, "rb").read()
+    assert raw[:8] == b"SAILJIT1"
+    rc, _, sha2 = _child_compile(dict(env, SAIL_HIPRTC=str(tmp_path / "none.so")), cache, masks)  # no compiler needed
+    assert rc == 0 and sha2 == sha1
+    bad = bytearray(raw)
+    bad[len(bad) // 2] ^= 0xFF
+    open(path, "wb").write(bytes(bad))
+    rc, msg, _ = _child_compile(dict(env, SAIL_HIPRTC=str(tmp_path / "none.so")), cache, masks)
+    assert rc != 0 and "dlmopen" in msg  # the corrupted object is not loaded: a compiler would be needed
+    rc, _, sha3 = _child_compile(env, cache, masks)
+    assert rc == 0 and sha3 == sha1 and open(path, "rb").read() == raw
+
+
+def test_prebuild_fills_the_shipped_cache_layout(tmp_path, fixtures):
+    """sail_jit_prebuild derives the spec a default context would (the frozen scenes: rows, pre-cull and room forms)
+    and writes its code object into the given directory"""
+    for name in ("C1", "C4"):
+        d = tmp_path / name
+        assert capi.jit_prebuild(fixtures["scenes"][name], cache_dir=str(d))
+        files = os.listdir(d)
+        assert len(files) == 1 and open(d / files[0], "rb").read(8) == b"SAILJIT1"
+
+
+@pytest.mark.gpu
+def test_box_compiler_matches_precompiled_kernels(tmp_path, fixtures, product_kernels):
+    """on the GPU box itself, the hipRTC the library opens there compiles the all-plugin, room and
+    Cornell sets to exactly the precompiled kernels' instructions (no disk cache: compiled in this process)"""
+    capi.set_jit_cache("")
+    try:
+        test_all_plugin_jit_equals_precompiled_generic(tmp_path, product_kernels)
+        test_room_form_of_the_room_set_equals_precompiled_room_kernel(tmp_path, product_kernels)
+        test_cornell_set_flat_form_equals_precompiled_cornell_kernel(tmp_path, fixtures, product_kernels)
+    finally:
+        capi.set_jit_cache(None)
+
+
+def test_two_precull_compiles_in_one_process(tmp_path):
+    """Regression: with one thread per background build, the second pre-cull-form compile of a process faulted inside
+    hipRTC (found on the GPU box, reproduced here); builds now share one long-lived worker thread. No caches."""
+    env = dict(os.environ, AMD_COMGR_CACHE="0")
     child = (
         "import ctypes, sys\n"
         f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
         "from sail_amd import capi\n"
-        "lib = capi.load(); pl = capi.Plugins(0x206, 6, 0, 0); n = ctypes.c_size_t(0)\n"
-        "rc = lib.sail_jit_compile(ctypes.byref(pl), 0, None, 0, None, ctypes.byref(n))\n"
-        "print(rc, lib.sail_last_error(None).decode())\n")
-    env = dict(os.environ, SAIL_HIPRTC=str(tmp_path / "missing" / "libhiprtc.so.7"))
-    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr[-2000:]
-    rc, msg = r.stdout.strip().split(" ", 1)
-    assert int(rc) != 0 and "dlmopen" in msg, r.stdout
+        "capi.set_jit_cache('')\n"
+        "lib = capi.load(); n = ctypes.c_size_t(0)\n"
+        "for masks in ((0xFFFFFFFF,) * 4, (0x206, 6, 0, 0)):\n"
+        "    pl = capi.Plugins(*masks)\n"
+        "    print(lib.sail_jit_compile(ctypes.byref(pl), 1, None, 0, None, ctypes.byref(n)), flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.split() == ["0", "0"]

@@ -40,7 +40,15 @@ def main():
     per = {k.replace("SQ_INSTS_VALU_", "").lower(): c[k] * 64 / segs for k in CLASSES if k in c}
     total = c["SQ_INSTS_VALU"] * 64 / segs
     per["other (moves, selects, compares, min/max, bit ops, lane ops)"] = total - sum(per.values())
-    rec = {"kernel": sorted(kernels)[0] if len(kernels) == 1 else sorted(kernels), "workload": workload,
+    ids = set()  # the profiled kernel's build identity, from each pass's bench line (roofline.kernel_id)
+    for p in ("mix1", "mix2"):
+        try:
+            with open(os.path.join(pdir, p + ".log")) as f:
+                ids |= {json.loads(x)["roofline"].get("kernel_id") for x in f if x.startswith("{") and '"roofline"' in x}
+        except OSError:
+            ids.add(None)
+    rec = {"kernel": sorted(kernels)[0] if len(kernels) == 1 else sorted(kernels),
+           "kernel_id": ids.pop() if len(ids) == 1 else None, "workload": workload,
            "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
            "source": "tools/pmc_mix.sh (rocprofv3 --pmc, two passes, kernel-trace only), mean per dispatch",
            "dispatch_mean_ns": durs, "counters": c,

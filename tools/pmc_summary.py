@@ -44,13 +44,25 @@ def main():
             c.update(vals)
             passes[p] = meta
     kernels = sorted({k for m in passes.values() for k in m["kernels"]})
+    # the build identity of the profiled kernel, from the bench line each pass printed (roofline.kernel_id): bench.py
+    # matches a summary to a kernel by it, so every pass must have profiled the same build
+    ids = set()
+    for p in passes:
+        try:
+            with open(os.path.join(pdir, p + ".log")) as f:
+                for line in f:
+                    if line.startswith("{") and '"roofline"' in line:
+                        ids.add(json.loads(line)["roofline"].get("kernel_id"))
+        except OSError:
+            ids.add(None)
+    kernel_id = ids.pop() if len(ids) == 1 else None
     fetch_b = c["FETCH_SIZE"] * 1024 * 2
     write_b = c["WRITE_SIZE"] * 1024
     alg = px * 32
     waves = c.get("SQ_WAVES", 0)
     segs = px * spp * bounces
     rec = {
-        "kernel": kernels[0] if len(kernels) == 1 else kernels, "workload": workload,
+        "kernel": kernels[0] if len(kernels) == 1 else kernels, "kernel_id": kernel_id, "workload": workload,
         "passes": passes, "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
         "hbm": {"fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
                 "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,

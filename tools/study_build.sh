@@ -11,7 +11,7 @@ COMMON="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize
 mkdir -p sail_amd/lib/variants
 for name in "$@"; do
   d=sail_amd/build/study/$name/csrc   # two levels below the root, like sail_amd/csrc: "../../include" resolves
-  rm -rf sail_amd/build/study/$name && mkdir -p $d && cp sail_amd/csrc/* $d/ && ln -sfn $ROOT/include sail_amd/build/study/include
+  rm -rf sail_amd/build/study/$name && mkdir -p $d && cp sail_amd/csrc/* $d/ && ln -sfn ../../../include sail_amd/build/study/include
   python3 tools/study/$name.py $d
   $HIPCC $COMMON -c $d/sail_trace.hip -o $d/sail_trace.o &
   $HIPCC $COMMON -c $d/sail_capi.cpp -o $d/sail_capi.o &
