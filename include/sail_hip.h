@@ -127,7 +127,10 @@ enum sail_debug_option {
   /* how long (ms) a launch waits for the scene's run-time kernel while it is still being built in the background; -1:
    * until it is built. Meanwhile the precompiled kernel of the scene's set renders, with the same results [0: never
    * wait, so Renderer.update / render stay interactive; the Python binding used by the tests and bench.py sets -1] */
-  SAIL_DEBUG_JIT_WAIT = 10
+  SAIL_DEBUG_JIT_WAIT = 10,
+  /* samples of each pixel in flight per workgroup of the run-time kernels: 1, 4 or 16 (the workgroup's lanes hold
+   * 256 / value pixels, 1,024 / value in the pre-cull form, each with `value` samples); 0 = the form's default */
+  SAIL_DEBUG_JIT_NS = 11
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 

@@ -156,6 +156,7 @@ struct sail_ctx {
   SailJitKernel jitK;
   std::string jitError;  // why the scene's run-time kernel failed (sail_get_kernel_info)
   int jitWait = 0;
+  int jitNs = 0;  // SAIL_DEBUG_JIT_NS: samples in flight of the run-time kernels (0: the form's default, jitNsFor)
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
   int lastJitMode = 0;
   uint64_t lastBuildId = 0;  // the run-time kernel's build identity (sail_get_kernel_info)
@@ -256,6 +257,11 @@ int jitWaves(int mode, int kernelSet) {
   if (mode == SAIL_JIT_MODE_ROOM) return kernelSet == SAIL_KSET_ROOM ? 7 : 8;
   return kernelSet == SAIL_KSET_CORNELL ? 8 : 6;
 }
+// Samples of each pixel in flight per workgroup of a run-time kernel, by form (traceTileCompact NS)
+int jitNsFor(int mode, int kernelSet) {
+  (void)mode; (void)kernelSet;
+  return 1;
+}
 // The run-time kernel spec of the context's scene under its switches, or false when none applies.
 // SAIL_DEBUG_JIT bits (include/sail_hip.h): 1 flat scenes outside the Cornell and room sets, 2 pre-cull scenes, 4 room-set
 // scenes, 8 the flat scenes of bit 1 in the room form, 16 flat scenes compiled for their rows as well (any flat scene).
@@ -284,6 +290,7 @@ bool jitSpecFor(const sail_ctx* c, SailJitSpec* out, int* mode) {
   spec.mode = m;
   spec.waves = jitWaves(m, set);
   spec.ldsFit = (m == SAIL_JIT_MODE_CULL && c->n <= SAIL_CULL_LDS_ROWS && c->tn <= SAIL_CULL_LDS_TP) ? 1 : 0;
+  spec.ns = c->jitNs ? c->jitNs : jitNsFor(m, set);
   if (rows && m != SAIL_JIT_MODE_CULL) {
     spec.rows = c->n;
     for (int i = 0; i < c->n; i++) spec.types[i] = c->primTypes[i];
@@ -735,6 +742,13 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     // Sample groups: a rank's share of a small frame is too few workgroups to fill the device (1/8 of 1080p
     // = 1,016 workgroups = 4 waves per SIMD); split the launch's samples over G workgroups per block so
     // that about 4 rounds of 7-wave-per-SIMD residency are queued, and add the staged samples in order.
+    const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
+    SailJitKernel jk;
+    int jmode = 0;
+    const bool jit = !wavefront && jitKernels(c, c->jitWait, &jk, &jmode);
+    // samples of each pixel in flight per workgroup (the run-time kernels' spec; the precompiled kernels hold one):
+    // NS times the workgroups of one sample in flight, each NS times shorter
+    const int ns = jit ? c->jitSpec.ns : 1;
     int G = 1;
     if (c->forceGroups > 0) {
       G = c->forceGroups;
@@ -745,13 +759,13 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       // rounds are queued (the grouped kernel is 1,024 threads too; measured 0.95 at N = 8 with 4 groups).
       // Round 3: more groups pay at any frame size (a shorter tail per launch); C4 at N = 1: G = 1 / 2 / 4 9.96 / 10.06
       // / 10.12 Gseg/s (gpurun_out/r03o), so about SAIL_CULL_GROUP_ROUNDS rounds are queued.
-      const double rounds = (double)owned * 4.0 / (double)(c->numCUs * 2);
+      const double rounds = (double)owned * 4.0 * ns / (double)(c->numCUs * 2);
       if (rounds < (double)c->cullGroupRounds) G = (int)ceil((double)c->cullGroupRounds / rounds);
     } else {
       // Round 3: splitting pays at full frame size too (shorter launch tails): C2 at N = 1 with G = 1 / 2 / 4 / 8 / 16
       // 89.3 / 89.7 / 90.9 / 91.6 / 91.4 Gseg/s, C5 87.0 / 89.3 / 90.9 / 91.6 / 91.9, C3 29.2 / 28.6 / 29.2 / 29.5 / 29.4;
       // at N = 8 (C2) G = 8 / 16 / 32 85 / 87 / 88 (gpurun_out/r03o). About 36 rounds of 7-wave residency are queued.
-      const long long waves = (long long)owned * 16 * 4;
+      const long long waves = (long long)owned * 16 * 4 * ns;
       const long long target = (long long)c->numCUs * 4 * 7 * c->flatGroupRounds;
       G = (int)((target + waves - 1) / waves);
     }
@@ -760,10 +774,6 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     if (nspp > stageSpp) G = 1;  // the stage would pass its cap
     A.groupSpp = (nspp + G - 1) / G;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
-    const bool wavefront = c->wavefront && A.kernelSet == SAIL_KSET_GENERIC && A.cullPrims;
-    SailJitKernel jk;
-    int jmode = 0;
-    const bool jit = !wavefront && jitKernels(c, c->jitWait, &jk, &jmode);
     A.groupHome = (jit ? jmode == SAIL_JIT_MODE_ROOM : SAIL_GROUP_HOME_FOR(A.kernelSet)) ? 1 : 0;
     A.stageStride = stageStride;
     const bool staged = A.sampleGroups > 1;
@@ -801,8 +811,10 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       if (jit) {
         void* args[] = {&A};
         const unsigned nt = jmode == SAIL_JIT_MODE_CULL ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips
-        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jk.grouped : jk.plain, (unsigned)(owned * 16 * A.sampleGroups) * 256u / nt, 1,
-                                        1, nt, 1, 1, 0, c->stream, args, nullptr));
+        const unsigned px = nt / (unsigned)ns;                            // pixels per workgroup
+        HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jk.grouped : jk.plain,
+                                        (unsigned)owned * (4096u / px) * (unsigned)A.sampleGroups, 1, 1, nt, 1, 1, 0,
+                                        c->stream, args, nullptr));
         c->lastJit = true;
         c->lastJitMode = jmode;
         c->lastBuildId = jk.buildId;
@@ -1184,6 +1196,11 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
     case SAIL_DEBUG_JIT: c->jit = value; break;
+    case SAIL_DEBUG_JIT_NS:
+      if (value != 0 && value != 1 && value != 4 && value != 16)
+        return fail(c, SAIL_E_INVALID, "sail_set_debug: samples in flight must be 0 (default), 1, 4 or 16");
+      c->jitNs = value;
+      break;
     case SAIL_DEBUG_JIT_WAIT:
       if (value < -1) return fail(c, SAIL_E_INVALID, "sail_set_debug: jit wait must be >= -1");
       c->jitWait = value;

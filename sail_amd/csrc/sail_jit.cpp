@@ -50,7 +50,7 @@ extern const int sail_jit_src_count;
 
 bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b) {
   const auto t = [](const SailJitSpec& x) {
-    return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.types[0], x.types[1], x.types[2],
+    return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.types[0], x.types[1], x.types[2],
                     x.types[3], x.types[4], x.types[5], x.types[6], x.types[7]);
   };
   return t(a) == t(b);
@@ -62,7 +62,7 @@ struct Key {
   SailJitSpec s;
   bool operator<(const Key& o) const {
     const auto t = [](const SailJitSpec& x) {
-      return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.types[0], x.types[1], x.types[2],
+      return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.types[0], x.types[1], x.types[2],
                       x.types[3], x.types[4], x.types[5], x.types[6], x.types[7]);
     };
     return t(s) < t(o.s);
@@ -102,9 +102,9 @@ std::string defsFor(const SailJitSpec& sp) {
            "#define SAIL_JIT 1\n#define SAIL_JIT_WAVES %d\n#define SAIL_JIT_CULL %d\n#define SAIL_JIT_FAM %d\n"
            "#define SAIL_JIT_KS 0x%xu\n#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n"
            "#define SAIL_JIT_NT %d\n#define SAIL_JIT_N %d\n#define SAIL_JIT_TYPES %s\n#define SAIL_JIT_LDSFIT %d\n"
-           "#define SAIL_JIT_TN %d\n#include \"sail_trace.hip\"\n",
+           "#define SAIL_JIT_TN %d\n#define SAIL_JIT_NS %d\n#include \"sail_trace.hip\"\n",
            sp.waves, sp.mode == 1, sp.mode == 2, sp.ks, sp.km, sp.kt, sp.kl, sp.mode == 1 ? 1024 : 256, sp.rows,
-           sp.rows ? types.c_str() : "0", sp.ldsFit, sp.tn);
+           sp.rows ? types.c_str() : "0", sp.ldsFit, sp.tn, sp.ns);
   return defs;
 }
 
@@ -292,7 +292,8 @@ bool validSpec(const SailJitSpec& sp, std::string* err) {
   bool ok = sp.mode >= 0 && sp.mode <= 2 && sp.waves >= 1 && sp.waves <= 8 && sp.rows >= 0 && sp.rows <= kSailJitMaxRows &&
             !(sp.mode == 1 && sp.rows) &&  // the pre-cull kernels sweep candidates, not rows
             (sp.ldsFit == 0 || (sp.ldsFit == 1 && sp.mode == 1)) &&
-            (sp.tn == 0 || (sp.tn >= 1 && sp.tn <= kSailJitMaxFlatTp && sp.mode != 1 && sp.rows > 0));
+            (sp.tn == 0 || (sp.tn >= 1 && sp.tn <= kSailJitMaxFlatTp && sp.mode != 1 && sp.rows > 0)) &&
+            (sp.ns == 1 || sp.ns == 4 || sp.ns == 16);
   for (int i = 0; ok && i < sp.rows; i++) ok = sp.types[i] >= 1 && sp.types[i] <= 9 && ((sp.ks >> sp.types[i]) & 1u);
   if (!ok) *err = "invalid kernel specialisation";
   return ok;

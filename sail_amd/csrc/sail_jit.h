@@ -13,6 +13,7 @@ struct SailJitSpec {
   int rows = 0;                             // > 0: the scene's row count, with each row's shape id in types
   int ldsFit = 0;                           // pre-cull: the scene's tables fit the LDS copies (SAIL_CULL_LDS_*)
   int tn = 0;                               // flat forms with rows: the texParams row count (LDS copies), 0 = none
+  int ns = 1;                               // samples of each pixel in flight per workgroup (1, 4, 16: traceTileCompact)
   int types[kSailJitMaxRows] = {};
 };
 bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b);

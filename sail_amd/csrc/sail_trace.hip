@@ -1610,10 +1610,19 @@ D void accumulateSample(float4& acc, V3 e, const SailSample& S, int mode) {
 // launches (one workgroup per block, every sample) are a separate compile-time instance, so they carry none of
 // the group bookkeeping in registers (sample groups add VGPR/SGPR spills to the flat kernels otherwise).
 struct TileWork { int ownedTile, sub, kBeg, kEnd, bid; };
-// NT-thread workgroups cover 16 x NT/16 pixel blocks, 4096 / NT of them per 64x64 tile
-template <bool GROUPED, int NT = 256>
+// A workgroup's pixel block: PX pixels (NT threads / NS samples in flight per pixel), BW x BH, 4096 / PX per 64x64 tile:
+// 16 x NT/16 strips with one sample in flight (NT = 256: 16 x 16; the pre-cull kernels' 1,024: 16 x 64), square blocks
+// otherwise (8 x 8 or 4 x 4 pixels x 4 or 16 samples)
+template <int PX> struct BlockGeo {
+  static constexpr int kBW = PX >= 256 ? 16 : (PX == 64 ? 8 : 4);
+  static constexpr int kBH = PX / kBW;
+  static constexpr int kPerRow = 64 / kBW;  // blocks per tile row
+  static constexpr int kPer = 4096 / PX;     // blocks per tile
+  static_assert(kBW * kBH == PX && PX >= 16 && 4096 % PX == 0 && kBW * kPerRow == 64, "pixel block shape");
+};
+template <bool GROUPED, int PX = 256>
 D TileWork tileWork(const SailTraceArgs& A) {
-  constexpr int kPer = 4096 / NT;
+  constexpr int kPer = BlockGeo<PX>::kPer;
   TileWork w;
   if (GROUPED) {
     const int nb = A.ownedTiles * kPer;
@@ -1629,19 +1638,18 @@ D TileWork tileWork(const SailTraceArgs& A) {
   w.ownedTile = w.bid / kPer; w.sub = w.bid % kPer;
   return w;
 }
-// The staged radiance of sample k at lane li of block bid (groups after the first; the first group, which holds
-// the launch's first samples, adds its own to the accumulator directly): stage planes 3k..3k+2, in the 256-thread
-// (16 x 16 block) slot order
-// sail_accum_kernel reads -- slot (ownedTile * 16 + block16) * 256 + (y mod 16) * 16 + (x mod 16) -- whatever NT is
-template <int NT = 256>
-D void stageSample(const SailTraceArgs& A, int k, int bid, int li, V3 e) {
+// The staged radiance of sample k at pixel p of block bid (groups after the first; the first group, which holds
+// the launch's first samples, adds its own to the accumulator directly): stage planes 3k..3k+2, in the slot order
+// sail_accum_kernel reads -- slot (ownedTile * 16 + block16) * 256 + (y mod 16) * 16 + (x mod 16) -- whatever the block
+template <int PX = 256>
+D void stageSample(const SailTraceArgs& A, int k, int bid, int p, V3 e) {
+  using G = BlockGeo<PX>;
   size_t slot;
-  if (NT == 256) {
-    slot = (size_t)bid * 256 + li;
-  } else {  // a 16 x NT/16 strip: sub-block column (bid mod 4), rows (bid / 4 mod kPer/4) * NT/16 + li / 16
-    constexpr int kPer = 4096 / NT;
-    const int ownedTile = bid / kPer, sub = bid % kPer;
-    const int ly = (sub >> 2) * (NT / 16) + (li >> 4), lx = (sub & 3) * 16 + (li & 15);
+  if (PX == 256 && G::kBW == 16) {
+    slot = (size_t)bid * 256 + p;
+  } else {
+    const int ownedTile = bid / G::kPer, sub = bid % G::kPer;
+    const int ly = (sub / G::kPerRow) * G::kBH + p / G::kBW, lx = (sub % G::kPerRow) * G::kBW + p % G::kBW;
     slot = ((size_t)ownedTile * 16 + (size_t)((ly >> 4) * 4 + (lx >> 4))) * 256 + (size_t)((ly & 15) * 16 + (lx & 15));
   }
   // three planes per sample (12 B per pixel instead of a float4's 16)
@@ -1704,9 +1712,17 @@ constexpr int kFlatTp = SAIL_JIT_TN;
 constexpr int kFlatTp = 0;
 #endif
 constexpr int kPrioMixed = 2;
-template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM>
+// NS samples of each pixel in flight per workgroup (1, 4 or 16): the workgroup's NT lanes hold NT / NS pixels x NS samples
+// (lane li: sample slot li / PX of pixel li % PX), so one workgroup finishes a launch's samples of its block NS times
+// sooner. The short units end a launch with a short tail without splitting the samples over workgroups (sample groups:
+// every sample's radiance staged in HBM and added in order by sail_accum_kernel); each pixel's NS radiances of a step
+// wait in LDS and its lane adds them in sample order, so the sums are those of one sample at a time, bit for bit.
+template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM, int NS = 1>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
-  static_assert(NT == 256 || NT == 128 || NT == 512 || NT == 1024, "16 x NT/16 pixel blocks");
+  static_assert(NT == 256 || NT == 1024, "256- or 1,024-thread workgroups");
+  static_assert(NS == 1 || NS == 4 || NS == 16, "samples in flight");
+  constexpr int kPX = NT / NS;  // pixels per workgroup
+  using G = BlockGeo<kPX>;
   constexpr int kKeys = 64;                // key = 1 + type * 5 + material category (types 0..9) < 64
   constexpr int kPack = CULL ? 1 : 2;
   constexpr bool kE4 = !CULL;
@@ -1733,15 +1749,19 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr bool kSort1 = CULL || FAM;  // sort the paths at the first bounce too
   __shared__ int sCnt2[twoBar ? 2 : 1][kKeys];  // [0] alone in the three-barrier sort
   __shared__ int sStart[twoBar ? 1 : kKeys + 1];
-  const TileWork tw = tileWork<GROUPED, NT>(A);
+  const TileWork tw = tileWork<GROUPED, kPX>(A);
   const int ownedTile = tw.ownedTile;
   if (ownedTile >= A.ownedTiles) return;  // uniform over the workgroup
   const int sub = tw.sub;
   const int tile = A.rank + ownedTile * A.world;
   const int tx = tile % A.tilesX, ty = tile / A.tilesX;
   const int li = threadIdx.x, lane = li & 63, wave = li >> 6;
-  const int x0 = tx * 64 + (sub & 3) * 16, y0 = ty * 64 + (sub >> 2) * (NT / 16);
-  const int x = x0 + (li & 15), y = y0 + (li >> 4);
+  const int x0 = tx * 64 + (sub % G::kPerRow) * G::kBW, y0 = ty * 64 + (sub / G::kPerRow) * G::kBH;
+  // a path's home slot (the lane it started on) names its pixel and its sample slot
+  auto homeX = [&](int h) { return x0 + (h % kPX) % G::kBW; };
+  auto homeY = [&](int h) { return y0 + (h % kPX) / G::kBW; };
+  const int mySlot = li / kPX;
+  const int x = homeX(li), y = homeY(li);
   const bool valid = x < A.W && y < A.H;   // ragged tiles: invalid lanes still serve migrated paths
 
   Ctx c;
@@ -1793,6 +1813,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
     }
   }
   int ph = 0;
+  // the seeds of the step's NS samples (NS > 1: a gathered path reads its own)
+  __shared__ float sSeed[NS];
+  if (NS > 1 && li < NS) sSeed[li] = constRow<SailSample>(A.samples, min(tw.kBeg + li, tw.kEnd - 1)).seed;
   __syncthreads();
   // sort key: the winning primitive row when there are few enough rows (no row reads for the key, and a wave's
   // paths share their primitive and material rows; C2 +3.7 %, C3 +1.2 %), else (shape type, material category).
@@ -1804,7 +1827,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   // a room-family kernel's first group accumulates its samples itself (SailTraceArgs.groupHome)
   constexpr bool kHome = FAM && !CULL;
   const bool home = !grouped || (kHome && tw.kBeg == 0);
-  float4 acc = (valid && home) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const bool pixLane = li < kPX;  // the lane that adds its pixel's samples (every lane when NS == 1)
+  float4 acc = (valid && home && pixLane) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
@@ -1818,11 +1842,14 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   for (int q = 0; q < 8; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
-  for (int k = tw.kBeg; k < tw.kEnd; k++) {
-    const SailSample& S = constRow<SailSample>(A.samples, k);
-    const bool aovSample = (A.aovN || A.aovP) && k == A.spp - 1;  // AOVs of the launch's last sample
-    bool alive = valid;
-    int pixel = li;
+  for (int k = tw.kBeg; k < tw.kEnd; k += NS) {
+    const int ks = k + mySlot;  // this lane's sample (NS == 1: k, uniform)
+    const bool inRange = NS == 1 || ks < tw.kEnd;
+    const SailSample& S = constRow<SailSample>(A.samples, NS == 1 ? k : (inRange ? ks : k));
+    const bool aovs = A.aovN || A.aovP;  // AOVs of the launch's last sample
+    bool alive = valid && inRange;
+    int pixel = li;  // the path's home slot
+    auto pathSeed = [&](int h) { if constexpr (NS == 1) return S.seed; else return sSeed[h / kPX]; };
     Ray ray;
     {
       const V3 d0 = v3(S.d[0][0], S.d[0][1], S.d[0][2]), d1 = v3(S.d[1][0], S.d[1][1], S.d[1][2]);
@@ -1841,8 +1868,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         if constexpr (!CULL) segs++;
         sw = sweepRay(c, ray, depth == 1);
         if (sw.best >= kMaxDistance) {  // the path leaves the scene: its radiance is final
-          if (depth == 1 && aovSample) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
-            const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
+          if (depth == 1 && aovs && k + pixel / kPX == A.spp - 1) {  // fstrace.glsl:15-16 with n = p = 0 (GLSL: undefined)
+            const size_t g = (size_t)homeY(pixel) * A.W + homeX(pixel);
             const V3 qn = v3s(0.0f) / 2.0f + 0.5f, qp = normalize(v3s(0.0f));
             if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
             if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
@@ -1953,20 +1980,21 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
           if (mixedW) __builtin_amdgcn_s_setprio(kPrioMixed);
           else __builtin_amdgcn_s_setprio(0);
         }
-        c.fcx = (float)(x0 + (pixel & 15)) + 0.5f;
-        c.fcy = (float)(y0 + (pixel >> 4)) + 0.5f;
+        c.fcx = (float)homeX(pixel) + 0.5f;
+        c.fcy = (float)homeY(pixel) + 0.5f;
+        const float seed = pathSeed(pixel) + (float)depth;
         const Hit ins = hitRecordU<true, FAM && !CULL>(c, ray, sw);
         PHASE_MARK(pc, 1);
-        if (depth == 1 && aovSample) {
-          const size_t g = (size_t)(y0 + (pixel >> 4)) * A.W + x0 + (pixel & 15);
+        if (depth == 1 && aovs && k + pixel / kPX == A.spp - 1) {
+          const size_t g = (size_t)homeY(pixel) * A.W + homeX(pixel);
           const V3 qn = ins.normal / 2.0f + 0.5f, qp = normalize(ins.hit);
           if (A.aovN) A.aovN[g] = make_float4(qn.x, qn.y, qn.z, 1.0f);
           if (A.aovP) A.aovP[g] = make_float4(qp.x, qp.y, qp.z, 1.0f);
         }
         V3 e = E_LOAD(pixel);
-        if (!(!CULL && depth == A.maxBounces && shadeLast(c, ins, S.seed + (float)depth, fpdf, e))) {
+        if (!(!CULL && depth == A.maxBounces && shadeLast(c, ins, seed, fpdf, e))) {
           if constexpr (kShCompact) {
-            shadeBounceT<true>(c, ins, ray, S.seed + (float)depth, fpdf, e, pc, &sp);
+            shadeBounceT<true>(c, ins, ray, seed, fpdf, e, pc, &sp);
             if (sp.pending) {  // both outcomes of e += (emission + (0 + light * f)) * throughput, as shadeBounce
               V3 dDark = v3s(0.0f), dLit = v3s(0.0f);
               dDark = dDark + v3s(0.0f) * sp.f;
@@ -1975,7 +2003,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
               e = e + (sp.emission + dDark) * sp.fpdfOld;
             }
           } else {
-            shadeBounce(c, ins, ray, S.seed + (float)depth, fpdf, e, pc);
+            shadeBounce(c, ins, ray, seed, fpdf, e, pc);
           }
         }
         E_STORE(pixel, e);
@@ -2026,14 +2054,25 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
     }
     __syncthreads();
-    if (valid) {
-      const V3 er = E_LOAD(li);
-      if (!home) stageSample<NT>(A, k, tw.bid, li, er);
-      else accumulateSample(acc, er, S, A.accumMode);
+    if constexpr (NS == 1) {
+      if (valid) {
+        const V3 er = E_LOAD(li);
+        if (!home) stageSample<kPX>(A, k, tw.bid, li, er);
+        else accumulateSample(acc, er, S, A.accumMode);
+      }
+    } else {
+      if (valid && pixLane) {  // the pixel's samples of this step, in sample order
+        for (int j = 0; j < NS && k + j < tw.kEnd; j++) {
+          const V3 er = E_LOAD(j * kPX + li);
+          if (!home) stageSample<kPX>(A, k + j, tw.bid, li, er);
+          else accumulateSample(acc, er, constRow<SailSample>(A.samples, k + j), A.accumMode);
+        }
+      }
+      if (li < NS && k + NS + li < tw.kEnd) sSeed[li] = constRow<SailSample>(A.samples, k + NS + li).seed;
     }
     __syncthreads();
   }
-  if (valid && home) A.accum[pixG] = acc;
+  if (valid && home && pixLane) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
   if (lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
@@ -2054,23 +2093,28 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
 // and threads per workgroup, chosen by the occupancy sweeps of DESIGN.md §5 (sail_launch_trace sizes the grids).
 // fam: the room family's choices for a flat kernel -- the two-barrier sort, the first sample group accumulating its
 // samples itself (SailTraceArgs.groupHome) and one box record for Cube and Cornellbox.
-#define SAIL_TRACE_KERNELS(name, waves, cull, ks, km, kt, kl, nt, gnt, fam)                                          \
+#define SAIL_TRACE_KERNELS_NS(name, waves, cull, ks, km, kt, kl, nt, gnt, fam, ns)                                 \
   extern "C" __global__ void __launch_bounds__(nt, waves) name(SailTraceArgs A) {                                \
-    traceTileCompact<cull, false, ks, km, kt, kl, nt, fam>(A);                                                   \
+    traceTileCompact<cull, false, ks, km, kt, kl, nt, fam, ns>(A);                                               \
   }                                                                                                              \
   extern "C" __global__ void __launch_bounds__(gnt, waves) name##_grouped(SailTraceArgs A) {                     \
-    traceTileCompact<cull, true, ks, km, kt, kl, gnt, fam>(A);                                                   \
+    traceTileCompact<cull, true, ks, km, kt, kl, gnt, fam, ns>(A);                                               \
   }
+#define SAIL_TRACE_KERNELS(name, waves, cull, ks, km, kt, kl, nt, gnt, fam) \
+  SAIL_TRACE_KERNELS_NS(name, waves, cull, ks, km, kt, kl, nt, gnt, fam, 1)
 #if defined(SAIL_JIT)
 // A per-plugin-set kernel compiled at run time by hipRTC (sail_jit.cpp), like the reference's per-scene program
 // (tracerConfig -> Generator.generate, src/scene/scene.js:70-112, src/shader/generator.js:107-123): the plugin masks,
 // the pre-cull choice, the family and the launch bounds arrive as macros, and only this kernel pair is compiled.
+#ifndef SAIL_JIT_NS
+#define SAIL_JIT_NS 1
+#endif
 #if SAIL_JIT_CULL
-SAIL_TRACE_KERNELS(sail_trace_kernel_cull_jit, SAIL_JIT_WAVES, true, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
-                   SAIL_JIT_NT, SAIL_JIT_NT, false)
+SAIL_TRACE_KERNELS_NS(sail_trace_kernel_cull_jit, SAIL_JIT_WAVES, true, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
+                      SAIL_JIT_NT, SAIL_JIT_NT, false, SAIL_JIT_NS)
 #else
-SAIL_TRACE_KERNELS(sail_trace_kernel_jit, SAIL_JIT_WAVES, false, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
-                   SAIL_JIT_NT, SAIL_JIT_NT, SAIL_JIT_FAM != 0)
+SAIL_TRACE_KERNELS_NS(sail_trace_kernel_jit, SAIL_JIT_WAVES, false, SAIL_JIT_KS, SAIL_JIT_KM, SAIL_JIT_KT, SAIL_JIT_KL,
+                      SAIL_JIT_NT, SAIL_JIT_NT, SAIL_JIT_FAM != 0, SAIL_JIT_NS)
 #endif
 #else
 // every plugin (any scene of fewer than 8 primitives outside the two sets below)

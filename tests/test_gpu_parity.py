@@ -878,3 +878,30 @@ def test_kernel_build_identity(gpu, fixtures):
     (n1, b1, j1), (n3, b3, _), (n0, b0, j0) = ids[("C1", False)], ids[("C3", False)], ids[("C1", True)]
     assert n1.startswith("sail_trace_kernel_jit") and b1 == j1 and b1 != b3
     assert n0.startswith("sail_trace_kernel_cornell") and b0 != b1 and j0 == "0" * 16
+
+
+@pytest.mark.parametrize("name,W,H,spp,B", [("C1", 37, 21, 7, 6), ("C3", 40, 36, 5, 6), ("C4", 36, 20, 5, 6),
+                                            ("ALL", 33, 17, 3, 5)])
+@pytest.mark.parametrize("ns", [4, 16])
+def test_samples_in_flight_bit_exact(gpu, fixtures, name, W, H, spp, B, ns):
+    """SAIL_DEBUG_JIT_NS: run-time kernels whose workgroups hold NS samples of 256 / NS pixels (1,024 / NS in the
+    pre-cull form) -- each pixel's samples of a step added in sample order -- equal the oracle bit for bit: ragged frames,
+    sample counts that are not a multiple of NS, 1 and 3 sample groups, the running-mean and 8-bit modes, and the AOVs
+    of the launch's last sample"""
+    sc = fixtures["scenes"][name]
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    masks = capi.plugin_masks(sc["plugins"])
+    for groups, mode in ((1, capi.ACCUM_SUM), (3, capi.ACCUM_SUM), (1, capi.ACCUM_MIX), (2, capi.ACCUM_COMPAT8)):
+        ctx = capi.Context(W, H, flags=capi.FLAG_AOV, debug={capi.DEBUG_JIT_NS: ns, capi.DEBUG_SAMPLE_GROUPS: groups})
+        try:
+            ctx.set_accum_mode(mode)
+            ctx.set_scene_dict(sc)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            assert ctx.kernel_name().startswith(("sail_trace_kernel_jit", "sail_trace_kernel_cull_jit")), ctx.kernel_name()
+            got = ctx.read_accum()
+            _, gn, gp = ctx.readback(aov=True)
+        finally:
+            ctx.close()
+        want, wn, wp = oracle.render(sc, masks, W, H, inv, seeds, sc["eye"], B, accum_mode=mode, aov=True)
+        assert bit_equal(got, want).all(), (groups, mode)
+        assert bit_equal(gn, wn).all() and bit_equal(gp, wp).all(), (groups, mode)

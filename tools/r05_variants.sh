@@ -1,0 +1,26 @@
+#!/bin/bash
+# The round-5 variant comparisons (profiles/r05_*.jsonl), one named step each, run through gpurun:
+#   bash tools/r05_variants.sh ns ...
+# Each step: tools/variant_bench.py <scene> name=lib[:debug option=value,...] (two alternating rounds, bit-identity
+# against the first variant checked), output under gpurun_out/r05v/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r05v; mkdir -p $O
+V=sail_amd/lib/variants
+vb() {  # vb <out> <timeout> <scene> <specs...>
+  local out=$1 t=$2; shift 2
+  VARIANT_ROUNDS=${VARIANT_ROUNDS:-2} timeout -k 10 $t python -u tools/variant_bench.py "$@" > $O/$out.jsonl 2>&1 || { tail $O/$out.jsonl; exit 3; }
+  cut -c1-170 $O/$out.jsonl
+}
+for step in "$@"; do
+  echo "== $step"
+  case $step in
+    ns)  # samples of each pixel in flight per workgroup of the run-time kernels (SAIL_DEBUG_JIT_NS 11)
+      for sc in C1 C3; do vb ns_$sc 400 $sc ns1=main:11=1 ns4=main:11=4 ns16=main:11=16; done
+      VARIANT_SPP=64 vb ns_C4 600 C4 ns1=main:11=1 ns4=main:11=4 ns16=main:11=16 ;;
+    ns_groups)  # the same with sample groups off (no stage at all)
+      for sc in C1 C3; do vb nsg_$sc 400 $sc ns1g1=main:11=1,4=1 ns4g1=main:11=4,4=1 ns16g1=main:11=16,4=1; done ;;
+    *) echo "unknown step $step"; exit 1 ;;
+  esac
+done
+echo "variants ok"

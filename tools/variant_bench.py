@@ -51,6 +51,7 @@ def main():
     sail_amd/lib/libsail_hip.so) with sail_set_debug switches; without specs, every sail_amd/lib/variants/*.so."""
     scene = sys.argv[1] if len(sys.argv) > 1 else "C1"
     W, H, B, spp = (3840, 2160, 12, 8) if scene == "C4" else (1920, 1080, 8, 128)
+    spp = int(os.environ.get("VARIANT_SPP", spp))
     with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
         sc = json.load(f)[scene]
     specs = []
