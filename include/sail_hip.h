@@ -130,7 +130,10 @@ enum sail_debug_option {
   SAIL_DEBUG_JIT_WAIT = 10,
   /* samples of each pixel in flight per workgroup of the run-time kernels: 1, 4 or 16 (the workgroup's lanes hold
    * 256 / value pixels, 1,024 / value in the pre-cull form, each with `value` samples); 0 = the form's default */
-  SAIL_DEBUG_JIT_NS = 11
+  SAIL_DEBUG_JIT_NS = 11,
+  /* threads per workgroup of the run-time kernels: 128, 256, 512 or 1024 (the path sort's pool); 0 = the form's own
+   * [0: 256 flat, 1,024 pre-cull] */
+  SAIL_DEBUG_JIT_NT = 12
 };
 int sail_set_debug(sail_ctx* ctx, int option, int value);
 

@@ -29,6 +29,7 @@ DEBUG_GROUP_ROUNDS = 7
 DEBUG_CULL_GROUP_ROUNDS = 8
 DEBUG_JIT = 9
 DEBUG_JIT_WAIT = 10  # ms a launch waits for the scene's run-time kernel (-1: until built; the C ABI's default is 0)
+DEBUG_JIT_NT = 12  # threads per workgroup of the run-time kernels (0: the form's own)
 DEBUG_JIT_NS = 11  # samples of each pixel in flight per workgroup of the run-time kernels (0: the form's default)
 KERNEL_JIT_NONE, KERNEL_JIT_PENDING, KERNEL_JIT_READY, KERNEL_JIT_FAILED = 0, 1, 2, 3
 JIT_MODE_FLAT, JIT_MODE_CULL, JIT_MODE_ROOM = 0, 1, 2  # sail_jit_compile kernel forms (include/sail_hip.h)

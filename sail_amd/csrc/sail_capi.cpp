@@ -156,6 +156,7 @@ struct sail_ctx {
   SailJitKernel jitK;
   std::string jitError;  // why the scene's run-time kernel failed (sail_get_kernel_info)
   int jitWait = 0;
+  int jitNt = 0;  // SAIL_DEBUG_JIT_NT: threads per workgroup of the run-time kernels (0: the form's own)
   int jitNs = 0;  // SAIL_DEBUG_JIT_NS: samples in flight of the run-time kernels (0: the form's default, jitNsFor)
   bool lastJit = false;  // the last trace launch ran a run-time compiled kernel (sail_kernel_name)
   int lastJitMode = 0;
@@ -257,10 +258,19 @@ int jitWaves(int mode, int kernelSet) {
   if (mode == SAIL_JIT_MODE_ROOM) return kernelSet == SAIL_KSET_ROOM ? 7 : 8;
   return kernelSet == SAIL_KSET_CORNELL ? 8 : 6;
 }
-// Samples of each pixel in flight per workgroup of a run-time kernel, by form (traceTileCompact NS)
+// Workgroup shape of a run-time kernel by form (profiles/r05_ns_*.jsonl, r05_nt*_C1.jsonl; 1080p / 4K, 64-sample
+// launches, bit-identical): the Cornell form at 512 threads holding 16 samples of 32 pixels (C1 98.6 Gseg/s against 97.5-98.1
+// at 256 threads x 1 sample with 8 staged sample groups: no stage and no sail_accum_kernel at full frame; 512 x 1 sample,
+// staged, 98.8-99.0); the room and pre-cull forms at their 256 / 1,024 threads holding 4 samples (C3 +1.2 %, C4 +0.8 %;
+// 16 samples C3 -0.4 %, C4 -1.3 %; C3 at 128 / 512 threads -9 % / -4 %, C4 at 512 -62 %: its LDS tables then
+// leave room for too few workgroups).
 int jitNsFor(int mode, int kernelSet) {
-  (void)mode; (void)kernelSet;
+  if (mode == SAIL_JIT_MODE_FLAT && kernelSet == SAIL_KSET_CORNELL) return 16;
+  if (mode == SAIL_JIT_MODE_ROOM || mode == SAIL_JIT_MODE_CULL) return 4;
   return 1;
+}
+int jitNtFor(int mode, int kernelSet) {
+  return (mode == SAIL_JIT_MODE_FLAT && kernelSet == SAIL_KSET_CORNELL) ? 512 : 0;
 }
 // The run-time kernel spec of the context's scene under its switches, or false when none applies.
 // SAIL_DEBUG_JIT bits (include/sail_hip.h): 1 flat scenes outside the Cornell and room sets, 2 pre-cull scenes, 4 room-set
@@ -291,6 +301,8 @@ bool jitSpecFor(const sail_ctx* c, SailJitSpec* out, int* mode) {
   spec.waves = jitWaves(m, set);
   spec.ldsFit = (m == SAIL_JIT_MODE_CULL && c->n <= SAIL_CULL_LDS_ROWS && c->tn <= SAIL_CULL_LDS_TP) ? 1 : 0;
   spec.ns = c->jitNs ? c->jitNs : jitNsFor(m, set);
+  spec.nt = c->jitNt ? c->jitNt : jitNtFor(m, set);
+  if (sailJitThreads(spec) / spec.ns < 16) spec.ns = 4;  // at least 16 pixels per workgroup
   if (rows && m != SAIL_JIT_MODE_CULL) {
     spec.rows = c->n;
     for (int i = 0; i < c->n; i++) spec.types[i] = c->primTypes[i];
@@ -810,7 +822,7 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
     } else {
       if (jit) {
         void* args[] = {&A};
-        const unsigned nt = jmode == SAIL_JIT_MODE_CULL ? 1024u : 256u;  // the pre-cull kernels' 16 x 64 strips
+        const unsigned nt = (unsigned)sailJitThreads(c->jitSpec);
         const unsigned px = nt / (unsigned)ns;                            // pixels per workgroup
         HIPCHK(c, hipModuleLaunchKernel(A.sampleGroups > 1 ? jk.grouped : jk.plain,
                                         (unsigned)owned * (4096u / px) * (unsigned)A.sampleGroups, 1, 1, nt, 1, 1, 0,
@@ -1196,6 +1208,11 @@ int sail_set_debug(sail_ctx* c, int option, int value) {
     case SAIL_DEBUG_SAMPLE_GROUPS: c->forceGroups = value; break;
     case SAIL_DEBUG_WAVEFRONT: c->wavefront = value; break;
     case SAIL_DEBUG_JIT: c->jit = value; break;
+    case SAIL_DEBUG_JIT_NT:
+      if (value != 0 && value != 128 && value != 256 && value != 512 && value != 1024)
+        return fail(c, SAIL_E_INVALID, "sail_set_debug: threads per workgroup must be 0 (default), 128, 256, 512 or 1024");
+      c->jitNt = value;
+      break;
     case SAIL_DEBUG_JIT_NS:
       if (value != 0 && value != 1 && value != 4 && value != 16)
         return fail(c, SAIL_E_INVALID, "sail_set_debug: samples in flight must be 0 (default), 1, 4 or 16");

@@ -48,9 +48,10 @@ extern const char* const sail_jit_src_names[];
 extern const char* const sail_jit_src_texts[];
 extern const int sail_jit_src_count;
 
+int sailJitThreads(const SailJitSpec& s) { return s.nt ? s.nt : (s.mode == 1 ? 1024 : 256); }
 bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b) {
   const auto t = [](const SailJitSpec& x) {
-    return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.types[0], x.types[1], x.types[2],
+    return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.nt, x.types[0], x.types[1], x.types[2],
                     x.types[3], x.types[4], x.types[5], x.types[6], x.types[7]);
   };
   return t(a) == t(b);
@@ -62,7 +63,7 @@ struct Key {
   SailJitSpec s;
   bool operator<(const Key& o) const {
     const auto t = [](const SailJitSpec& x) {
-      return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.types[0], x.types[1], x.types[2],
+      return std::tie(x.ks, x.km, x.kt, x.kl, x.mode, x.waves, x.rows, x.ldsFit, x.tn, x.ns, x.nt, x.types[0], x.types[1], x.types[2],
                       x.types[3], x.types[4], x.types[5], x.types[6], x.types[7]);
     };
     return t(s) < t(o.s);
@@ -103,7 +104,7 @@ std::string defsFor(const SailJitSpec& sp) {
            "#define SAIL_JIT_KS 0x%xu\n#define SAIL_JIT_KM 0x%xu\n#define SAIL_JIT_KT 0x%xu\n#define SAIL_JIT_KL 0x%xu\n"
            "#define SAIL_JIT_NT %d\n#define SAIL_JIT_N %d\n#define SAIL_JIT_TYPES %s\n#define SAIL_JIT_LDSFIT %d\n"
            "#define SAIL_JIT_TN %d\n#define SAIL_JIT_NS %d\n#include \"sail_trace.hip\"\n",
-           sp.waves, sp.mode == 1, sp.mode == 2, sp.ks, sp.km, sp.kt, sp.kl, sp.mode == 1 ? 1024 : 256, sp.rows,
+           sp.waves, sp.mode == 1, sp.mode == 2, sp.ks, sp.km, sp.kt, sp.kl, sailJitThreads(sp), sp.rows,
            sp.rows ? types.c_str() : "0", sp.ldsFit, sp.tn, sp.ns);
   return defs;
 }
@@ -293,7 +294,8 @@ bool validSpec(const SailJitSpec& sp, std::string* err) {
             !(sp.mode == 1 && sp.rows) &&  // the pre-cull kernels sweep candidates, not rows
             (sp.ldsFit == 0 || (sp.ldsFit == 1 && sp.mode == 1)) &&
             (sp.tn == 0 || (sp.tn >= 1 && sp.tn <= kSailJitMaxFlatTp && sp.mode != 1 && sp.rows > 0)) &&
-            (sp.ns == 1 || sp.ns == 4 || sp.ns == 16);
+            (sp.ns == 1 || sp.ns == 4 || sp.ns == 16) &&
+            (sp.nt == 0 || sp.nt == 128 || sp.nt == 256 || sp.nt == 512 || sp.nt == 1024) && sailJitThreads(sp) / sp.ns >= 16;
   for (int i = 0; ok && i < sp.rows; i++) ok = sp.types[i] >= 1 && sp.types[i] <= 9 && ((sp.ks >> sp.types[i]) & 1u);
   if (!ok) *err = "invalid kernel specialisation";
   return ok;

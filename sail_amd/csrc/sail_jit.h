@@ -14,9 +14,11 @@ struct SailJitSpec {
   int ldsFit = 0;                           // pre-cull: the scene's tables fit the LDS copies (SAIL_CULL_LDS_*)
   int tn = 0;                               // flat forms with rows: the texParams row count (LDS copies), 0 = none
   int ns = 1;                               // samples of each pixel in flight per workgroup (1, 4, 16: traceTileCompact)
+  int nt = 0;                               // threads per workgroup (128 .. 1,024); 0 = the form's own (1,024 pre-cull, 256)
   int types[kSailJitMaxRows] = {};
 };
 bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b);
+int sailJitThreads(const SailJitSpec& s);  // threads per workgroup of the spec's kernels
 
 // A loaded kernel pair and where its code object came from.
 struct SailJitKernel {

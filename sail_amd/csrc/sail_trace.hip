@@ -141,8 +141,8 @@ D Ray mkRay(V3 o, V3 d) {
 #define SAIL_PHASE_TIMING 0
 #endif
 #if SAIL_PHASE_TIMING
-__device__ unsigned long long g_sailPhase[8];
-struct PhaseClock { unsigned long long t, acc[8]; };
+__device__ unsigned long long g_sailPhase[12];
+struct PhaseClock { unsigned long long t, acc[12]; };
 #define PHASE_MARK(pc, k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); (pc).acc[k] += now_ - (pc).t; (pc).t = now_; } while (0)
 #else
 struct PhaseClock {};
@@ -1614,7 +1614,7 @@ struct TileWork { int ownedTile, sub, kBeg, kEnd, bid; };
 // 16 x NT/16 strips with one sample in flight (NT = 256: 16 x 16; the pre-cull kernels' 1,024: 16 x 64), square blocks
 // otherwise (8 x 8 or 4 x 4 pixels x 4 or 16 samples)
 template <int PX> struct BlockGeo {
-  static constexpr int kBW = PX >= 256 ? 16 : (PX == 64 ? 8 : 4);
+  static constexpr int kBW = PX >= 128 ? 16 : (PX >= 32 ? 8 : 4);
   static constexpr int kBH = PX / kBW;
   static constexpr int kPerRow = 64 / kBW;  // blocks per tile row
   static constexpr int kPer = 4096 / PX;     // blocks per tile
@@ -1719,7 +1719,7 @@ constexpr int kPrioMixed = 2;
 // wait in LDS and its lane adds them in sample order, so the sums are those of one sample at a time, bit for bit.
 template <bool CULL, bool GROUPED, uint32_t KS, uint32_t KM, uint32_t KT, uint32_t KL, int NT, bool FAM, int NS = 1>
 __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
-  static_assert(NT == 256 || NT == 1024, "256- or 1,024-thread workgroups");
+  static_assert(NT == 128 || NT == 256 || NT == 512 || NT == 1024, "workgroups of 2, 4, 8 or 16 waves");
   static_assert(NS == 1 || NS == 4 || NS == 16, "samples in flight");
   constexpr int kPX = NT / NS;  // pixels per workgroup
   using G = BlockGeo<kPX>;
@@ -1839,7 +1839,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   unsigned long long segsW = 0;
   PhaseClock pc;
 #if SAIL_PHASE_TIMING
-  for (int q = 0; q < 8; q++) pc.acc[q] = 0;
+  for (int q = 0; q < 12; q++) pc.acc[q] = 0;
   pc.t = __builtin_amdgcn_s_memtime();
 #endif
   for (int k = tw.kBeg; k < tw.kEnd; k += NS) {
@@ -1912,7 +1912,9 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       // between the scan and the scatter; the counts alternate between two buffers, the one just read being
       // cleared by wave 0 after the scatter barrier, two bounces before it is counted into again
       if (alive) rank = atomicAdd(&sCnt2[ph][key], 1);
+      PHASE_MARK(pc, 7);  // rank atomics
       __syncthreads();
+      PHASE_MARK(pc, 8);  // barrier 1 wait
       {
         const int v = sCnt2[ph][lane];
         const int incl = waveScanIncl(v);
@@ -1920,13 +1922,17 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         const int start = __shfl(incl - v, key, 64);
         if (alive) scatterTo(start + rank);
       }
+      PHASE_MARK(pc, 9);  // scan + scatter
       __syncthreads();
+      PHASE_MARK(pc, 10);  // barrier 2 wait
       if (wave == 0) sCnt2[ph][lane] = 0;
       ph ^= 1;
       } else {
       int* const sCnt = sCnt2[0];
       if (alive) rank = atomicAdd(&sCnt[key], 1);
+      PHASE_MARK(pc, 7);  // rank atomics
       __syncthreads();
+      PHASE_MARK(pc, 8);  // barrier 1 wait
       if (wave == 0) {
         const int v = sCnt[lane];
         const int incl = waveScanIncl(v);
@@ -1934,10 +1940,14 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         if (lane == 63) sStart[kKeys] = incl;
         sCnt[lane] = 0;
       }
+      PHASE_MARK(pc, 9);  // scan
       __syncthreads();
+      PHASE_MARK(pc, 10);  // barrier 2 wait
       nAlive = sStart[kKeys];
       if (alive) scatterTo(sStart[key] + rank);
+      PHASE_MARK(pc, 9);  // scatter
       __syncthreads();
+      PHASE_MARK(pc, 10);  // barrier 3 wait
       }
       alive = li < nAlive;
       }
@@ -1945,7 +1955,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       sp.pending = false;
       V3 eLit = v3s(0.0f);
       int keyG = 0;  // the gathered path's sort key
-      PHASE_MARK(pc, 7);
+      PHASE_MARK(pc, 9);
       if (alive) {
         if (!sortNow) {
           keyG = key;
@@ -2071,11 +2081,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       if (li < NS && k + NS + li < tw.kEnd) sSeed[li] = constRow<SailSample>(A.samples, k + NS + li).seed;
     }
     __syncthreads();
+    PHASE_MARK(pc, 11);  // sample end: barriers, accumulation / staging
   }
   if (valid && home && pixLane) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING
   if (lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
+    for (int q = 0; q < 12; q++) atomicAdd(&g_sailPhase[q], pc.acc[q]);
 #endif
   if (A.segCounter) {
     unsigned long long v = segsW;
@@ -2556,10 +2567,10 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
 extern const int sail_trace_phase_timing = SAIL_PHASE_TIMING;
 #if SAIL_PHASE_TIMING
 // phase-timing readout for the variant harness (tools/variant_bench.py --phases)
-extern "C" int sail_phase_read(unsigned long long out[8], int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+extern "C" int sail_phase_read(unsigned long long out[12], int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 12 * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_sailPhase), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -622,7 +622,7 @@ def test_phase_timing_build_bit_exact(gpu, fixtures, monkeypatch, name, W, H, sp
     lib.sail_phase_read.restype = ctypes.c_int
     lib.sail_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     monkeypatch.setattr(capi, "_lib", lib)
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 12)()
     assert lib.sail_phase_read(buf, 1) == 0
     sc = fixtures["scenes"][name]
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
@@ -882,8 +882,8 @@ def test_kernel_build_identity(gpu, fixtures):
 
 @pytest.mark.parametrize("name,W,H,spp,B", [("C1", 37, 21, 7, 6), ("C3", 40, 36, 5, 6), ("C4", 36, 20, 5, 6),
                                             ("ALL", 33, 17, 3, 5)])
-@pytest.mark.parametrize("ns", [4, 16])
-def test_samples_in_flight_bit_exact(gpu, fixtures, name, W, H, spp, B, ns):
+@pytest.mark.parametrize("ns,nt", [(4, 0), (16, 0), (16, 512), (4, 128), (1, 512)])
+def test_samples_in_flight_bit_exact(gpu, fixtures, name, W, H, spp, B, ns, nt):
     """SAIL_DEBUG_JIT_NS: run-time kernels whose workgroups hold NS samples of 256 / NS pixels (1,024 / NS in the
     pre-cull form) -- each pixel's samples of a step added in sample order -- equal the oracle bit for bit: ragged frames,
     sample counts that are not a multiple of NS, 1 and 3 sample groups, the running-mean and 8-bit modes, and the AOVs
@@ -892,7 +892,8 @@ def test_samples_in_flight_bit_exact(gpu, fixtures, name, W, H, spp, B, ns):
     inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
     masks = capi.plugin_masks(sc["plugins"])
     for groups, mode in ((1, capi.ACCUM_SUM), (3, capi.ACCUM_SUM), (1, capi.ACCUM_MIX), (2, capi.ACCUM_COMPAT8)):
-        ctx = capi.Context(W, H, flags=capi.FLAG_AOV, debug={capi.DEBUG_JIT_NS: ns, capi.DEBUG_SAMPLE_GROUPS: groups})
+        dbg = {capi.DEBUG_JIT_NS: ns, capi.DEBUG_JIT_NT: nt, capi.DEBUG_SAMPLE_GROUPS: groups}
+        ctx = capi.Context(W, H, flags=capi.FLAG_AOV, debug=dbg)
         try:
             ctx.set_accum_mode(mode)
             ctx.set_scene_dict(sc)

@@ -17,7 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from sail_amd import capi  # noqa: E402
 
-PHASES = ["sweep", "hit record", "shading frame", "hash RNG", "BSDF sample", "light + shadow", "next ray", "sort + barriers"]
+PHASES = ["sweep", "hit record", "shading frame", "hash RNG", "BSDF sample", "light + shadow", "next ray",
+          "sort: rank atomics", "sort: barrier 1 wait", "sort: scan + scatter", "sort: barrier 2 (+3) wait",
+          "sample end: barriers + accumulation"]
 
 
 def main():
@@ -29,7 +31,7 @@ def main():
     lib.sail_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     with open(os.path.join(ROOT, "sail_amd", "scenes", "frozen.json")) as f:
         frozen = json.load(f)
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 12)()
     for name in scenes:
         sc = frozen[name]
         W, H, B, spp = (3840, 2160, 12, 8) if name == "C4" else (1920, 1080, 8, 64)

@@ -20,6 +20,14 @@ for step in "$@"; do
       VARIANT_SPP=64 vb ns_C4 600 C4 ns1=main:11=1 ns4=main:11=4 ns16=main:11=16 ;;
     ns_groups)  # the same with sample groups off (no stage at all)
       for sc in C1 C3; do vb nsg_$sc 400 $sc ns1g1=main:11=1,4=1 ns4g1=main:11=4,4=1 ns16g1=main:11=16,4=1; done ;;
+    nt)  # threads per workgroup of the run-time kernels (SAIL_DEBUG_JIT_NT 12): the path sort's pool and barrier width
+      vb nt_C1 400 C1 nt256=main nt128=main:12=128 nt512=main:12=512
+      vb nt_C3 500 C3 nt256ns4=main:11=4 nt128ns4=main:12=128,11=4 nt512ns4=main:12=512,11=4 nt128=main:12=128
+      VARIANT_SPP=64 vb nt_C4 600 C4 nt1024ns4=main:11=4 nt512ns4=main:12=512,11=4 nt512=main:12=512 ;;
+    nt_c1)  # wider sort pools for the Cornell form, with samples in flight
+      vb nt2_C1 500 C1 nt512=main:12=512 nt1024=main:12=1024 nt512ns4=main:12=512,11=4 nt1024ns4=main:12=1024,11=4 nt1024ns16=main:12=1024,11=16 ;;
+    nt_c1b)  # the Cornell form at 512 threads with 1 / 4 / 16 samples in flight (16: no sample stage)
+      vb nt3_C1 500 C1 nt512=main:12=512 nt512ns16=main:12=512,11=16 nt256ns16=main:11=16 nt256=main:12=256,11=1 ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
