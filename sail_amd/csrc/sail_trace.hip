@@ -1525,14 +1525,25 @@ D bool shadeLast(const Ctx& c, const Hit& ins, float seed, const V3& fpdf, V3& e
 // shade() (path.glsl:1-14) + the bounce bookkeeping of trace() (path.glsl:27-36): radiance, throughput, next ray
 // A lit matte path's light sample whose shadow test is left to a later pass (the wavefront split, SAIL_DEBUG_WAVEFRONT):
 // everything the radiance update e += (emission + light * f) * fpdf needs once the shadow ray's answer is known
-struct ShadowPending { bool pending; V3 contrib, toLight, hit, f, emission, fpdfOld; };
-template <bool DEFER>
-D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, ShadowPending* sp);
+// e holds the dark outcome of the radiance update (the light blocked); eLit the unblocked one, to be taken when the
+// shadow ray from `hit` along `toLight` is not blocked. Both are shadeBounce's e += (emission + (0 + light * f)) * fpdf.
+struct ShadowPending { bool pending; V3 toLight, hit, eLit; };
+// DEFER: a lit matte path's shadow ray is handed to onShadow(hit, toLight, eLit) where it is made (so that nothing of it
+// stays live through the rest of the bounce) and e takes the blocked outcome
+template <bool DEFER, class OnShadow>
+D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, OnShadow&& onShadow);
 D void shadeBounce(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc) {
-  shadeBounceT<false>(c, ins, ray, seed, fpdf, e, pc, nullptr);
+  shadeBounceT<false>(c, ins, ray, seed, fpdf, e, pc, [](const V3&, const V3&, const V3&) {});
 }
-template <bool DEFER>
-D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, ShadowPending* sp) {
+// the deferred shadow ray into a ShadowPending (the pre-cull kernel's compacted shadow rays, the wavefront split)
+D void shadeBounceP(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, ShadowPending& sp) {
+  sp.pending = false;
+  shadeBounceT<true>(c, ins, ray, seed, fpdf, e, pc, [&](const V3& hit, const V3& toLight, const V3& eLit) {
+    sp.pending = true; sp.hit = hit; sp.toLight = toLight; sp.eLit = eLit;
+  });
+}
+template <bool DEFER, class OnShadow>
+D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf, V3& e, PhaseClock& pc, OnShadow&& onShadow) {
   {
     // shade()
     // box faces have axis-aligned unit dpdu: dot == 1 exactly, sqrt(1) == 1 and v / 1 == v bit for bit
@@ -1560,26 +1571,23 @@ D void shadeBounceT(const Ctx& c, const Hit& ins, Ray& ray, float seed, V3& fpdf
     const V3 wi = ins.axis ? localToWorldX(wiL, ins.normal, ss, ts) : localToWorld(wiL, ins.normal, ss, ts);
     PHASE_MARK(pc, 4);  // BSDF sample
     V3 direct = v3s(0.0f);
-    bool deferE = false;
-    if (DEFER) sp->pending = false;
     if (isBlack(ins.emission) && ins.matCategory == SAIL_MATTE) {
       if (c.kLights == 0) {  // no light plugin: lightSample is 0, and 0 + 0 * f == fma(f, 0, 0) bit for bit
         direct = v3(fma_(f.x, 0.0f, 0.0f), fma_(f.y, 0.0f, 0.0f), fma_(f.z, 0.0f, 0.0f));
-      } else if (DEFER) {  // lightSample's light prep now, its shadow test and the radiance update in the shadow pass
+      } else if (DEFER) {  // lightSample's light prep now; its shadow test later picks one of the two outcomes
         const LightPrep lp = lightPrep(c, ins, u2);
         if (lp.lit && !posZero3(lp.contrib)) {
-          sp->pending = true; sp->contrib = lp.contrib; sp->toLight = lp.toLight; sp->hit = ins.hit; sp->f = f;
-          sp->emission = ins.emission; sp->fpdfOld = fpdf;
-          deferE = true;
-        } else {
-          direct = direct + v3s(0.0f) * f;
+          V3 dLit = v3s(0.0f);
+          dLit = dLit + lp.contrib * f;
+          onShadow(ins.hit, lp.toLight, e + (ins.emission + dLit) * fpdf);
         }
+        direct = direct + v3s(0.0f) * f;  // the dark outcome (light 0), or no shadow ray at all
       } else {
         direct = direct + lightSample(c, ins, u2) * f;
       }
     }
     PHASE_MARK(pc, 5);  // light sample + shadow ray
-    if (!deferE) {
+    {
       const V3 sh = ins.emission + direct;
       e = e + sh * fpdf;
     }
@@ -1889,6 +1897,12 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       int rank = 0;
       int nAlive;
       // a path's state into sorted slot d
+      // after the scatter a lane's old path state is dead (a live lane gathers a new one, a dead lane reads none): say
+      // so, or the compiler keeps it live across the sort for the lanes that gather nothing
+      auto dropState = [&]() {
+        ray.o = v3s(0.0f); ray.d = v3s(0.0f); ray.rx = ray.ry = ray.rz = 0.0f;
+        fpdf = v3s(0.0f); sw.best = 0.0f; sw.bi = 0; pixel = 0;
+      };
       auto scatterTo = [&](int d) {
         if constexpr (kPack == 2) {
           sSt4[0][d] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
@@ -1921,6 +1935,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         nAlive = __builtin_amdgcn_readlane(incl, 63);
         const int start = __shfl(incl - v, key, 64);
         if (alive) scatterTo(start + rank);
+        dropState();
       }
       PHASE_MARK(pc, 9);  // scan + scatter
       __syncthreads();
@@ -1945,6 +1960,7 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       PHASE_MARK(pc, 10);  // barrier 2 wait
       nAlive = sStart[kKeys];
       if (alive) scatterTo(sStart[key] + rank);
+      dropState();
       PHASE_MARK(pc, 9);  // scatter
       __syncthreads();
       PHASE_MARK(pc, 10);  // barrier 3 wait
@@ -2004,14 +2020,8 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
         V3 e = E_LOAD(pixel);
         if (!(!CULL && depth == A.maxBounces && shadeLast(c, ins, seed, fpdf, e))) {
           if constexpr (kShCompact) {
-            shadeBounceT<true>(c, ins, ray, seed, fpdf, e, pc, &sp);
-            if (sp.pending) {  // both outcomes of e += (emission + (0 + light * f)) * throughput, as shadeBounce
-              V3 dDark = v3s(0.0f), dLit = v3s(0.0f);
-              dDark = dDark + v3s(0.0f) * sp.f;
-              dLit = dLit + sp.contrib * sp.f;
-              eLit = e + (sp.emission + dLit) * sp.fpdfOld;
-              e = e + (sp.emission + dDark) * sp.fpdfOld;
-            }
+            shadeBounceP(c, ins, ray, seed, fpdf, e, pc, sp);  // e: the dark outcome
+            eLit = sp.eLit;
           } else {
             shadeBounce(c, ins, ray, seed, fpdf, e, pc);
           }
@@ -2253,7 +2263,7 @@ extern "C" __global__ void __launch_bounds__(256) sail_wf_shade(SailTraceArgs A,
   const float seed = constRow<SailSample>(A.samples, k).seed + (float)depth;
   PhaseClock pc;
   ShadowPending sp;
-  shadeBounceT<true>(c, ins, ray, seed, fpdf, e, pc, &sp);
+  shadeBounceP(c, ins, ray, seed, fpdf, e, pc, sp);
   S.e[slot] = make_float4(e.x, e.y, e.z, 0.0f);
   S.f[slot] = make_float4(fpdf.x, fpdf.y, fpdf.z, 0.0f);
   S.o[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, 1.0f);
@@ -2261,27 +2271,18 @@ extern "C" __global__ void __launch_bounds__(256) sail_wf_shade(SailTraceArgs A,
   S.sp[0][slot] = make_float4(sp.hit.x, sp.hit.y, sp.hit.z, sp.pending ? 1.0f : 0.0f);
   if (sp.pending) {
     S.sp[1][slot] = make_float4(sp.toLight.x, sp.toLight.y, sp.toLight.z, 0.0f);
-    S.sp[2][slot] = make_float4(sp.contrib.x, sp.contrib.y, sp.contrib.z, 0.0f);
-    S.sp[3][slot] = make_float4(sp.f.x, sp.f.y, sp.f.z, 0.0f);
-    S.sp[4][slot] = make_float4(sp.emission.x, sp.emission.y, sp.emission.z, 0.0f);
-    S.sp[5][slot] = make_float4(sp.fpdfOld.x, sp.fpdfOld.y, sp.fpdfOld.z, 0.0f);
+    S.sp[2][slot] = make_float4(sp.eLit.x, sp.eLit.y, sp.eLit.z, 0.0f);
   }
 }
-// the deferred shadow tests (testShadow, shader.light.js:24-31) and the radiance update they held back:
-// direct = 0 + light * f, e = e + (emission + direct) * throughput, as shadeBounce writes it
+// the deferred shadow tests (testShadow, shader.light.js:24-31): the radiance holds the blocked outcome of the update,
+// replaced by the unblocked one (ShadowPending.eLit) when the ray is not blocked
 extern "C" __global__ void __launch_bounds__(256) sail_wf_shadow(SailTraceArgs A, SailWfState S) {
   const long long slot = (long long)blockIdx.x * 256 + threadIdx.x;
   const float4 h = S.sp[0][slot];
   if (h.w == 0.0f) return;
   const Ctx c = wfCtx(A);
-  const float4 tl = S.sp[1][slot], ct = S.sp[2][slot], ff = S.sp[3][slot], em = S.sp[4][slot], fo = S.sp[5][slot];
-  const V3 light = testShadow(c, mkRay(v3(h.x, h.y, h.z), v3(tl.x, tl.y, tl.z))) ? v3s(0.0f) : v3(ct.x, ct.y, ct.z);
-  V3 direct = v3s(0.0f);
-  direct = direct + light * v3(ff.x, ff.y, ff.z);
-  const V3 sh = v3(em.x, em.y, em.z) + direct;
-  const float4 ee = S.e[slot];
-  const V3 e = v3(ee.x, ee.y, ee.z) + sh * v3(fo.x, fo.y, fo.z);
-  S.e[slot] = make_float4(e.x, e.y, e.z, 0.0f);
+  const float4 tl = S.sp[1][slot], el = S.sp[2][slot];
+  if (!testShadow(c, mkRay(v3(h.x, h.y, h.z), v3(tl.x, tl.y, tl.z)))) S.e[slot] = make_float4(el.x, el.y, el.z, 0.0f);
 }
 // sample k's radiance into the accumulator (sample order: one launch per sample)
 extern "C" __global__ void __launch_bounds__(256) sail_wf_accum(SailTraceArgs A, SailWfState S, int k) {

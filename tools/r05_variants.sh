@@ -28,6 +28,8 @@ for step in "$@"; do
       vb nt2_C1 500 C1 nt512=main:12=512 nt1024=main:12=1024 nt512ns4=main:12=512,11=4 nt1024ns4=main:12=1024,11=4 nt1024ns16=main:12=1024,11=16 ;;
     nt_c1b)  # the Cornell form at 512 threads with 1 / 4 / 16 samples in flight (16: no sample stage)
       vb nt3_C1 500 C1 nt512=main:12=512 nt512ns16=main:12=512,11=16 nt256ns16=main:11=16 nt256=main:12=256,11=1 ;;
+    shdefer)  # the room form's shadow rays traced inside the next sort vs inside the shading (study build room_nodefer)
+      for sc in C3 UI AREA; do vb shdefer_$sc 400 $sc defer=main nodefer=$V/libsail_hip_room_nodefer.so; done ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done

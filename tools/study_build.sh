@@ -1,5 +1,5 @@
 #!/bin/sh
-# Study builds: a copy of sail_amd/csrc patched by tools/study/<name>.py (plain string replacements, committed), built
+# Study builds: a copy of sail_amd/csrc patched by tools/study.py <name> (string replacements catalogued in tools/studies.json), built
 # like the product into sail_amd/lib/variants/libsail_hip_<name>.so. The product sources are never edited; results of
 # a study are measured by tools/variant_bench.py and recorded in profiles/.
 # Usage: tools/study_build.sh name [name ...]
@@ -12,7 +12,7 @@ mkdir -p sail_amd/lib/variants
 for name in "$@"; do
   d=sail_amd/build/study/$name/csrc   # two levels below the root, like sail_amd/csrc: "../../include" resolves
   rm -rf sail_amd/build/study/$name && mkdir -p $d && cp sail_amd/csrc/* $d/ && ln -sfn ../../../include sail_amd/build/study/include
-  python3 tools/study/$name.py $d
+  python3 tools/study.py $name $d
   $HIPCC $COMMON -c $d/sail_trace.hip -o $d/sail_trace.o &
   $HIPCC $COMMON -c $d/sail_capi.cpp -o $d/sail_capi.o &
   $HIPCC $COMMON -c $d/sail_hostmath.cpp -o $d/sail_hostmath.o &
