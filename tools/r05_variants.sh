@@ -30,6 +30,14 @@ for step in "$@"; do
       vb nt3_C1 500 C1 nt512=main:12=512 nt512ns16=main:12=512,11=16 nt256ns16=main:11=16 nt256=main:12=256,11=1 ;;
     shdefer)  # the room form's shadow rays traced inside the next sort vs inside the shading (study build room_nodefer)
       for sc in C3 UI AREA; do vb shdefer_$sc 400 $sc defer=main nodefer=$V/libsail_hip_room_nodefer.so; done ;;
+    launder)  # per-lane pixel values recomputed per sample step (working tree) vs kept from the start (HEAD build) vs
+              # recomputed at the step's start only (study launder_start_only)
+      for sc in C1 C3; do vb launder_$sc 400 $sc cur=main head=$V/libsail_hip_head.so start=$V/libsail_hip_launder_start_only.so; done
+      VARIANT_SPP=64 vb launder_C4 600 C4 cur=main head=$V/libsail_hip_head.so start=$V/libsail_hip_launder_start_only.so ;;
+    cornell)  # the Cornell form's sort: two barriers (study cornell_twobar), sorted first bounce (cornell_sort1); and
+              # 128-sample launches
+      vb cornell_C1 500 C1 cur=main twobar=$V/libsail_hip_cornell_twobar.so sort1=$V/libsail_hip_cornell_sort1.so
+      VARIANT_LAUNCH=128 vb cornell_C1_l128 300 C1 cur128=main ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
