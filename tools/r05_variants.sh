@@ -38,6 +38,9 @@ for step in "$@"; do
               # 128-sample launches
       vb cornell_C1 500 C1 cur=main twobar=$V/libsail_hip_cornell_twobar.so sort1=$V/libsail_hip_cornell_sort1.so
       VARIANT_LAUNCH=128 vb cornell_C1_l128 300 C1 cur128=main ;;
+    groups)  # sample groups at the new workgroup shapes (SAIL_DEBUG_SAMPLE_GROUPS 4; default: sized by residency rounds)
+      vb groups_C3 500 C3 auto=main g1=main:4=1 g4=main:4=4
+      VARIANT_SPP=64 vb groups_C4 700 C4 auto=main g1=main:4=1 g4=main:4=4 ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done

@@ -14,6 +14,7 @@
 #   phases           tools/phase_profile.py with the phase-timing build (sail_amd/lib/libsail_hip_phase.so)
 #   jshost           the JS host bench (sail_amd/js/tools/bench_host.js)
 #   torchrun         bench.py under torch.distributed.run at N = 1
+#   jit_times        the run-time kernels' build latency per form, cold and warm disk cache
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=gpurun_out/${OUT:-session}
@@ -76,6 +77,9 @@ for step in "$@"; do
         --master-port 29517 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_torchrun.log \
         2> $OUT/bench_torchrun.err || { tail $OUT/bench_torchrun.err; exit 13; }
       cut -c1-300 $OUT/bench_torchrun.log ;;
+    jit_times)  # run-time kernel build latency per form, cold and warm (tools/jit_compile_times.py)
+      timeout -k 10 900 python -u tools/jit_compile_times.py > $OUT/jit_compile_times.jsonl 2> $OUT/jit_compile_times.err || { tail $OUT/jit_compile_times.err; exit 14; }
+      cat $OUT/jit_compile_times.jsonl ;;
     jshost)
       timeout -k 10 300 node sail_amd/js/tools/bench_host.js > $OUT/bench_js_host.json 2> $OUT/bench_js_host.err || exit 12
       cut -c1-300 $OUT/bench_js_host.json ;;
