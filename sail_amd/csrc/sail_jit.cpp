@@ -11,15 +11,15 @@
 // background build, and until its module is loaded the context launches the precompiled kernel of the scene's set (the
 // frames are bit-identical either way; tests/test_gpu_parity.py renders across the swap). Code objects are kept
 //  * per process, per (arch, spec); modules per (device, spec);
-//  * on disk, keyed by (arch, spec, the embedded sources' hash, the compile flags, the hipRTC version): the user's
+//  * on disk, keyed by (arch, spec, the embedded sources' hash, the compile flags, the compiler's version): the user's
 //    cache ($XDG_CACHE_HOME or $HOME/.cache, sail_amd/jit; sail_set_jit_cache) and a read-only cache shipped next to the
 //    library (sail_amd/lib/jit, filled at build time for the frozen scenes by sail_jit_prebuild).
 //
 // The compiler is the ROCm toolchain's own hipRTC (and the comgr it loads), opened in a link namespace of its own
 // (dlmopen): a process that loaded another HIP runtime first -- PyTorch ships hipRTC and comgr of an older ROCm under
 // the same sonames -- would otherwise compile with that one, and the kernels would differ from the precompiled ones
-// (tests/test_jit_compile.py checks instruction identity after importing torch). A hipRTC whose version differs from
-// the one this library was built with is refused (the precompiled kernels serve).
+// (tests/test_jit_compile.py checks instruction identity after importing torch). A code object produced by another
+// compiler than the one this library was built with is refused (sameCompiler; the precompiled kernels serve).
 #include <dlfcn.h>
 #include <pthread.h>
 #include <errno.h>
@@ -70,7 +70,7 @@ struct Key {
   }
 };
 
-uint64_t fnv(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+uint64_t fnv(const void* p, size_t n, uint64_t h = 14695981039346656037ull) {
   const unsigned char* b = static_cast<const unsigned char*>(p);
   for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
   return h;
@@ -199,7 +199,7 @@ void mkdirs(const std::string& dir) {
 // (arch, spec, flags, embedded sources, the compiler that built this library -- which is the only producer a code
 // object may come from, sameCompiler): no hipRTC is needed to look a code object up
 uint64_t cacheKey(const std::string& arch, const Key& k) {
-  uint64_t h = fnvStr("sailjit-v2", 1469598103934665603ull);
+  uint64_t h = fnvStr("sailjit-v2", 14695981039346656037ull);
   h = fnvStr(arch, h);
   h = fnvStr(defsFor(k.s), h);
   for (const char* o : kOpts) h = fnvStr(o, h);
@@ -434,6 +434,8 @@ std::shared_ptr<Entry> request(const std::string& arch, const Key& k, const std:
     e = slot;
     std::vector<char> code;
     const uint64_t key = cacheKey(arch, k);
+    if (getenv("SAIL_JIT_DEFS"))  // tooling (tools/isa.sh): the source prefix of this spec, to rebuild it with hipcc
+      fprintf(stderr, "sail_jit %s %s\n%s", arch.c_str(), hex16(key).c_str(), defsFor(k.s).c_str());
     if (const int from = cacheLookup(key, code)) {
       if (!extraDir.empty()) cacheWrite(extraDir, key, code);
       finish(*e, code, "", 0.0, from);

@@ -41,6 +41,9 @@ for step in "$@"; do
     groups)  # sample groups at the new workgroup shapes (SAIL_DEBUG_SAMPLE_GROUPS 4; default: sized by residency rounds)
       vb groups_C3 500 C3 auto=main g1=main:4=1 g4=main:4=4
       VARIANT_SPP=64 vb groups_C4 700 C4 auto=main g1=main:4=1 g4=main:4=4 ;;
+    recheck)  # samples in flight / workgroup width of the room and pre-cull forms after the shadow-record rework
+      vb recheck_C3 600 C3 ns4=main ns16=main:11=16 nt512ns4=main:12=512,11=4 nt512ns16=main:12=512,11=16 nt128ns4=main:12=128,11=4
+      VARIANT_SPP=64 vb recheck_C4 700 C4 ns4=main ns1=main:11=1 ns16=main:11=16 nt512ns4=main:12=512,11=4 ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
