@@ -6,7 +6,7 @@
 #   tests            pytest -m gpu (the driver's suite)              smoke       __graft_entry__.smoke()
 #   bench            bench.py C2 with the CPU baselines               bench_quick bench.py C2, no CPU baseline
 #   bench_c3|c4|c5   the config's full frame                          bench_rccl  C2 through the forced-RCCL branch
-#   prof_c2|c3|c4    rocprofv3 --kernel-trace --stats of the config's bench (C4 at 64 spp: one launch)
+#   prof_c2|c3|c4|c5 rocprofv3 --kernel-trace --stats of the config's bench (C4 at 64 spp: one launch)
 #   pmc_c2|c3|c4|c5  the four PMC passes of tools/pmc.sh, summarised into gpurun_out/summ/$TAG_pmc_summary_<cfg>.json
 #   mix_c2|c3        the VALU instruction-mix passes of tools/pmc_mix.sh, summarised the same way
 #   scale            the per-rank emulation of N = 1/2/4/8 (tools/scaling_probe.py) for C2..C5
@@ -54,6 +54,7 @@ for step in "$@"; do
     prof_c2) prof prof_c2 --steps 3 --warmup 1 --no-cpu-baseline || exit 6 ;;
     prof_c3) prof prof_c3 --config C3 --steps 1 --warmup 1 --no-cpu-baseline || exit 6 ;;
     prof_c4) prof prof_c4 --config C4 --steps 1 --warmup 1 --spp 64 --no-cpu-baseline || exit 6 ;;
+    prof_c5) prof prof_c5 --config C5 --steps 1 --warmup 1 --no-cpu-baseline || exit 6 ;;
     pmc_c2|pmc_c3|pmc_c4|pmc_c5)
       c=${step#pmc_}; cfg=$(echo $c | tr a-z A-Z)
       PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=64 bash tools/pmc.sh > /dev/null || exit 7  # one 64-spp launch
