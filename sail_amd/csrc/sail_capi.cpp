@@ -264,8 +264,20 @@ int jitWaves(int mode, int kernelSet) {
 // staged, 98.8-99.0); the room and pre-cull forms at their 256 / 1,024 threads holding 4 samples (C3 +1.2 %, C4 +0.8 %;
 // 16 samples C3 -0.4 %, C4 -1.3 %; C3 at 128 / 512 threads -9 % / -4 %, C4 at 512 -62 %: its LDS tables then
 // leave room for too few workgroups).
-int jitNsFor(int mode, int kernelSet) {
-  if (mode == SAIL_JIT_MODE_FLAT && kernelSet == SAIL_KSET_CORNELL) return 16;
+// The Cornell form's 16 samples in flight pay while the context's share of the frame queues enough workgroups: with a
+// small share (a rank of 8 or more, one eighth of 1080p) it holds 1 sample and the launch is split into staged sample
+// groups instead (C2 per GPU at N = 8: 95.4 Gseg/s against 92.1 with 16 samples and no groups, 91.4 with both; at
+// N = 4 95.2 against 94.9; profiles/r05_scale_ns_c2.jsonl, tools/scale_groups.sh).
+int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY);
+bool cornellShareLarge(const sail_ctx* c) {
+  int tx, ty;
+  const int owned = ownedTiles(c, &tx, &ty);
+  // residency rounds of 512-thread workgroups at 8 waves per SIMD (4,096 / 32 pixels = 128 workgroups per tile)
+  const double rounds = (double)owned * 128.0 / ((double)c->numCUs * 4.0);
+  return rounds >= 12.0;
+}
+int jitNsFor(const sail_ctx* c, int mode, int kernelSet) {
+  if (mode == SAIL_JIT_MODE_FLAT && kernelSet == SAIL_KSET_CORNELL) return cornellShareLarge(c) ? 16 : 1;
   if (mode == SAIL_JIT_MODE_ROOM || mode == SAIL_JIT_MODE_CULL) return 4;
   return 1;
 }
@@ -300,7 +312,7 @@ bool jitSpecFor(const sail_ctx* c, SailJitSpec* out, int* mode) {
   spec.mode = m;
   spec.waves = jitWaves(m, set);
   spec.ldsFit = (m == SAIL_JIT_MODE_CULL && c->n <= SAIL_CULL_LDS_ROWS && c->tn <= SAIL_CULL_LDS_TP) ? 1 : 0;
-  spec.ns = c->jitNs ? c->jitNs : jitNsFor(m, set);
+  spec.ns = c->jitNs ? c->jitNs : jitNsFor(c, m, set);
   spec.nt = c->jitNt ? c->jitNt : jitNtFor(m, set);
   if (sailJitThreads(spec) / spec.ns < 16) spec.ns = 4;  // at least 16 pixels per workgroup
   if (rows && m != SAIL_JIT_MODE_CULL) {
@@ -780,11 +792,17 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
       const long long waves = (long long)owned * 16 * 4 * ns;
       const long long target = (long long)c->numCUs * 4 * 7 * c->flatGroupRounds;
       G = (int)((target + waves - 1) / waves);
+      // the Cornell form holds 16 samples in flight only while its share queues enough workgroups (jitNsFor), and then
+      // runs unsplit: staged groups lost 2-3 % per GPU at N = 4 and 8 (profiles/r05_scale_groups_c2.jsonl)
+      if (ns >= 16) G = 1;
     }
     if (G > nspp) G = nspp;
     if (G < 1) G = 1;
     if (nspp > stageSpp) G = 1;  // the stage would pass its cap
     A.groupSpp = (nspp + G - 1) / G;
+    // whole steps of the workgroup's samples in flight: a group of 11 samples at 4 in flight would idle a quarter of
+    // the lanes in its last step (C4 per GPU at N = 2 and 4: 12.6 Gseg/s against 13.4, profiles/r05_scale_groups_c4.jsonl)
+    if (ns > 1 && A.groupSpp < nspp && c->forceGroups <= 0) A.groupSpp = ((A.groupSpp + ns - 1) / ns) * ns;
     A.sampleGroups = (nspp + A.groupSpp - 1) / A.groupSpp;
     A.groupHome = (jit ? jmode == SAIL_JIT_MODE_ROOM : SAIL_GROUP_HOME_FOR(A.kernelSet)) ? 1 : 0;
     A.stageStride = stageStride;
@@ -1370,6 +1388,7 @@ int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
     return fail(c, SAIL_E_INVALID, "sample partition needs SAIL_ACCUM_SUM");
   HIPCHK(c, hipSetDevice(c->device));
   c->rank = rank; c->world = world; c->partMode = mode;
+  refreshJit(c);  // the Cornell form's samples in flight follow the share of the frame (jitNsFor)
   return resetAccum(c);
 }
 
@@ -1821,7 +1840,13 @@ int sail_jit_prebuild(const float* objects, int n, const float* texparams, int t
   if (built) *built = 0;
   if (!jitSpecFor(&t, &spec, &mode)) return SAIL_OK;  // the scene gets no run-time kernel
   std::string err;
-  if (sail_jit_code_to_dir(arch, spec, dir, &err)) return fail(nullptr, SAIL_E_INVALID, "sail_jit_prebuild: %s", err.c_str());
+  // the Cornell form in both shapes: 16 samples in flight (a large share of the frame) and 1 (a rank of 8, jitNsFor)
+  const bool cornell = mode == SAIL_JIT_MODE_FLAT && kernelSetFor(&t) == SAIL_KSET_CORNELL;
+  for (int ns : {16, 1}) {
+    if (cornell) spec.ns = ns;
+    if (sail_jit_code_to_dir(arch, spec, dir, &err)) return fail(nullptr, SAIL_E_INVALID, "sail_jit_prebuild: %s", err.c_str());
+    if (!cornell) break;
+  }
   if (built) *built = 1;
   return SAIL_OK;
 }

@@ -880,6 +880,23 @@ def test_kernel_build_identity(gpu, fixtures):
     assert n0.startswith("sail_trace_kernel_cornell") and b0 != b1 and j0 == "0" * 16
 
 
+def test_cornell_form_follows_the_share_of_the_frame(gpu, fixtures):
+    """the Cornell form holds 16 samples in flight for a large share of the frame and 1 for a rank of 8 (sail_capi.cpp
+    jitNsFor): set_partition switches the run-time kernel, and back (both are in the cache shipped with the library)"""
+    sc = fixtures["scenes"]["C1"]
+    ctx = capi.Context(1920, 1080)
+    try:
+        ctx.set_scene_dict(sc)
+        ids = []
+        for world in (1, 8, 2, 1):
+            ctx.set_partition(0, world)
+            assert ctx.kernel_ready(-1)
+            ids.append(ctx.kernel_info()["jit_build_id"])
+        assert ids[0] == ids[2] == ids[3] != ids[1], ids
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("name,W,H,spp,B", [("C1", 37, 21, 7, 6), ("C3", 40, 36, 5, 6), ("C4", 36, 20, 5, 6),
                                             ("ALL", 33, 17, 3, 5)])
 @pytest.mark.parametrize("ns,nt", [(4, 0), (16, 0), (16, 512), (4, 128), (1, 512)])

@@ -2,7 +2,7 @@
 """Per-rank trace throughput for world sizes 1/2/4/8 emulated on one GPU (rank 0's and rank N-1's share only, no
 collective): predicts the strong-scaling efficiency of bench.py --gpus N before the reduce is added. A tile config
 renders the rank's tiles; a sample-split config (C5) renders its samples k = rank mod N of the whole frame.
-Usage: tools/scaling_probe.py [config] [spp] [--groups g] [--worlds 1,2,4,8]
+Usage: tools/scaling_probe.py [config] [spp] [--groups g] [--worlds 1,2,4,8] [--debug k=v,...]
 --groups g fixes the sample-group count (SAIL_DEBUG_SAMPLE_GROUPS) instead of the host's occupancy rule; --rounds /
 --cull-rounds change that rule's target (SAIL_DEBUG_GROUP_ROUNDS / SAIL_DEBUG_CULL_GROUP_ROUNDS)."""
 import argparse
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=0, help="SAIL_DEBUG_GROUP_ROUNDS (flat kernels)")
     ap.add_argument("--cull-rounds", type=int, default=0, help="SAIL_DEBUG_CULL_GROUP_ROUNDS")
     ap.add_argument("--lib", default=None, help="a variant build of libsail_hip.so (tools/build_variants.sh)")
+    ap.add_argument("--debug", default="", help="extra sail_set_debug options, k=v[,k=v...] (e.g. 11=4: SAIL_DEBUG_JIT_NS)")
     a = ap.parse_args()
     if a.lib:
         capi._lib = capi.load(a.lib)
@@ -47,6 +48,9 @@ def main():
                 ctx.set_debug(capi.DEBUG_GROUP_ROUNDS, a.rounds)
             if a.cull_rounds:
                 ctx.set_debug(capi.DEBUG_CULL_GROUP_ROUNDS, a.cull_rounds)
+            for kv in filter(None, a.debug.split(",")):
+                k, v = kv.split("=")
+                ctx.set_debug(int(k), int(v))
             ctx.set_scene_dict(sc)
             ctx.set_partition(rank, world, part)
             ctx.render_schedule(inv[:32], seeds[:32], sc["eye"], B)  # warm-up
@@ -72,7 +76,7 @@ def main():
             if base is None:
                 base = rate
             print(json.dumps({"lib": os.path.basename(a.lib) if a.lib else "main", "config": a.config, "partition": "tiles" if part == capi.PART_TILES else "samples",
-                              "spp": spp, "groups": a.groups or "auto", "rounds": a.rounds or a.cull_rounds or "default", "world": world, "rank": rank,
+                              "spp": spp, "groups": a.groups or "auto", "rounds": a.rounds or a.cull_rounds or "default", "debug": a.debug, "world": world, "rank": rank,
                               "share": round(share, 5), "s": round(best, 4), "launches": int(st.launches),
                               "Gseg_per_s_per_gpu": round(rate, 3), "vs_1gpu": round(rate / base, 3),
                               "frame_speedup_if_all_ranks_like_this": round(rate / base / share, 2)}), flush=True)
