@@ -213,6 +213,52 @@ def test_load_rejects_mismatched_checkpoints(gpu, fixtures):
         b.close()
 
 
+@pytest.mark.parametrize("call", ["set_scene", "set_accum_mode", "set_partition"])
+def test_half_loaded_checkpoint_abandoned_by_every_reset(gpu, fixtures, call):
+    """every multi-device call that restarts the accumulation abandons a half-loaded checkpoint, like
+    sail_reset: the frame is usable again, and a different checkpoint then loads part by part"""
+    sc = fixtures["scenes"]["C1"]
+    W, H, B = 24, 16, 3
+    inv, seeds = _sched(sc, W, H, 0, 3)
+    cks = []
+    for n in (2, 3):
+        a = capi.Context(W, H, devices=[0, 0])
+        try:
+            a.set_scene_dict(sc)
+            a.render_schedule(inv[:n], seeds[:n], sc["eye"], B)
+            cks.append(a.save())
+        finally:
+            a.close()
+    assert cks[0]["k"] != cks[1]["k"]
+    b = capi.Context(W, H, devices=[0, 0])
+    try:
+        b.set_scene_dict(sc)
+        out = np.zeros((H, W, 4), np.float32)
+        p0 = np.ascontiguousarray(cks[0]["parts"][0])
+        assert b.lib.sail_load_accum(b.h, 0, capi._ptr(p0), cks[0]["k"]) == 0
+        assert b.lib.sail_read_accum(b.h, capi._ptr(out)) == -4  # half loaded
+        if call == "set_scene":
+            b.set_scene_dict(sc)
+        elif call == "set_accum_mode":
+            b.set_accum_mode(capi.ACCUM_SUM)
+        else:
+            b.set_partition(0, 1, capi.PART_TILES)
+        assert b.lib.sail_read_accum(b.h, capi._ptr(out)) == 0
+        assert not out.any()  # restarted
+        for i, part in enumerate(cks[1]["parts"]):  # the other checkpoint, part by part
+            assert b.lib.sail_load_accum(b.h, i, capi._ptr(np.ascontiguousarray(part)), cks[1]["k"]) == 0
+        want = capi.Context(W, H)
+        try:
+            want.set_scene_dict(sc)
+            want.render_schedule(inv[:3], seeds[:3], sc["eye"], B)
+            ref = want.read_accum()
+        finally:
+            want.close()
+        assert bit_equal(b.read_accum(), ref).all()
+    finally:
+        b.close()
+
+
 # ---- the sail_render queue (one-sample frames launched together) -------------------------------------------------
 @pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_render_queue_bit_exact_and_batched(gpu, fixtures, devices):

@@ -44,6 +44,9 @@ for step in "$@"; do
     recheck)  # samples in flight / workgroup width of the room and pre-cull forms after the shadow-record rework
       vb recheck_C3 600 C3 ns4=main ns16=main:11=16 nt512ns4=main:12=512,11=4 nt512ns16=main:12=512,11=16 nt128ns4=main:12=128,11=4
       VARIANT_SPP=64 vb recheck_C4 700 C4 ns4=main ns1=main:11=1 ns16=main:11=16 nt512ns4=main:12=512,11=4 ;;
+    sched)  # the run-time kernels under other LLVM machine-scheduler strategies (studies sched_*)
+      for sc in C1 C3; do vb sched_$sc 500 $sc cur=main ilp=$V/libsail_hip_sched_ilp.so memclause=$V/libsail_hip_sched_memclause.so iterilp=$V/libsail_hip_sched_iterilp.so; done
+      VARIANT_SPP=64 vb sched_C4 700 C4 cur=main ilp=$V/libsail_hip_sched_ilp.so memclause=$V/libsail_hip_sched_memclause.so iterilp=$V/libsail_hip_sched_iterilp.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
