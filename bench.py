@@ -252,7 +252,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--launch-spp", type=int, default=64)
+    ap.add_argument("--launch-spp", type=int, default=0,
+                    help="samples per kernel launch (default 0: the library's choice by kernel form, sail_set_launch_samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c1-full", action="store_true", help="skip the ~30 s full C1 render of the CPU baseline")
     ap.add_argument("--force-rccl", action="store_true",
@@ -309,7 +310,8 @@ def main():
     for opt, val in debug.items():
         ctx.set_debug(opt, val)
     ctx.set_scene_dict(sc)
-    ctx.set_launch_samples(args.launch_spp)
+    if args.launch_spp:
+        ctx.set_launch_samples(args.launch_spp)
     # the scene's run-time kernel (built in the background at set_scene; from the cache shipped beside the library for
     # the frozen scenes) before the warm-up, so every timed launch runs it
     ctx.kernel_ready(-1)
@@ -375,14 +377,18 @@ def main():
             tiles_px = 0
             for t in range(0, tx * ty, ngpu):
                 tiles_px += min(64, W - (t % tx) * 64) * min(64, H - (t // tx) * 64)
-        segs_per_launch = tiles_px * args.launch_spp * B
+        # samples per launch: the library's choice by kernel form unless --launch-spp fixed it (each step renders spp
+        # samples in launches of at most that many; stats count every device's launches)
+        per_dev = launches / (args.gpus if multi else 1) / args.steps
+        launch_spp = args.launch_spp or int(round(spp / per_dev))
+        segs_per_launch = tiles_px * launch_spp * B
         ops_seg, ops_live = ops_per_segment(sc, masks, mvp, W, H, B)
         achieved_tflops = ops_seg * segs_per_launch / avg_launch_s / 1e12
         achieved_live = ops_live * segs_per_launch / avg_launch_s / 1e12
         hbm_gbs = (tiles_px * 32) / avg_launch_s / 1e9   # float4 accumulator read + write per pixel per launch
         kinfo = ctx.kernel_info()
         kernel_id = f"{kinfo['name']}@{kinfo['build_id']}"
-        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, args.launch_spp, B, kernel_id)
+        traffic, traffic_src, pmc = profiled_traffic(cfg["workload"], tiles_px, launch_spp, B, kernel_id)
         rec = {
             "metric": "Msamples/s (paths x bounces) at 1920x1080 Cornell box" if args.config == "C2"
                       else f"Msamples/s (paths x bounces), {cfg['workload']}",
@@ -399,7 +405,7 @@ def main():
             "data": f"synthetic: frozen {cfg['desc']} scene rows (SURVEY §8(d), JS API == reference serializer), "
                     "deterministic sample schedule",
             "config": {"workload": cfg["workload"] + ("_wavefront_split" if args.wavefront else ""), "width": W, "height": H, "bounces": B, "spp": spp,
-                       "launch_spp": args.launch_spp, "partition": f"tiles64x{ngpu}",
+                       "launch_spp": launch_spp, "partition": f"tiles64x{ngpu}",
                        "processes": "one per GPU" if world > 1 else ("one (multi-device context)" if multi else "one"), "segments_per_step": W * H * spp * B,
                        **({"debug": debug} if debug else {})},
             "roofline": {

@@ -98,7 +98,7 @@ int sail_update_objects(sail_ctx* ctx, const float* objects, int n);
 
 int sail_set_accum_mode(sail_ctx* ctx, int mode);        /* resets accumulation */
 int sail_set_partition(sail_ctx* ctx, int rank, int world, int mode);
-int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch (default 64) */
+int sail_set_launch_samples(sail_ctx* ctx, int spp_per_launch); /* samples per kernel launch; 0 (default) = by kernel form: 1024 for the Cornell form with 16 samples in flight, else 64 */
 /* Test / study switches (no reference counterpart; none changes a result, which the parity suite checks).
  * The product's defaults are the values in brackets. */
 enum sail_debug_option {

@@ -169,7 +169,9 @@ struct sail_ctx {
   size_t stageBytes = 0;
   int accumMode = SAIL_ACCUM_SUM;
   int rank = 0, world = 1, partMode = SAIL_PART_TILES;
-  int launchSpp = 64;   // samples per launch: 64 measured C2 +0.7 %, C3 +0.5 %, C4/C5 +-0.2 % over 32 (profiles/r04_launch_spp*)
+  // samples per launch (sail_set_launch_samples); 0 = by form (launchSamples): 64 measured C2 +0.7 %, C3 +0.5 %, C4/C5
+  // +-0.2 % over 32 (profiles/r04_launch_spp*)
+  int launchSpp = 0;
   uint64_t k = 0;  // global sample index of the next sample (the reference's sampleCount)
   uint64_t samplesThisRank = 0;
   uint64_t nominalSegments = 0;
@@ -362,6 +364,15 @@ bool jitKernels(sail_ctx* c, int wait_ms, SailJitKernel* k, int* mode) {
   *k = c->jitK;
   *mode = c->jitMode;
   return true;
+}
+// Samples per launch when the host has not fixed them: the Cornell form holding 16 samples in flight runs a whole
+// 1,024-sample frame in one launch (its waves live 16 times longer, so their per-wave start -- the spill stores of the
+// loop-invariant registers among it -- is paid 16 times less often: C1 Gseg/s at 64 / 128 / 256 / 1,024 samples per
+// launch 97.26 / 97.73 / 97.99 / 98.36, profiles/r05_launch_*.jsonl); everything else 64 (sample groups stage a launch's
+// samples, which a larger launch would push past the stage's cap).
+int launchSamples(const sail_ctx* c) {
+  if (c->launchSpp > 0) return c->launchSpp;
+  return (c->jitHave && c->jitState != SAIL_KERNEL_JIT_FAILED && c->jitSpec.ns >= 16) ? 1024 : 64;
 }
 int ownedTiles(const sail_ctx* c, int* tilesX, int* tilesY) {
   const int tx = (c->W + 63) / 64, ty = (c->H + 63) / 64;
@@ -743,8 +754,9 @@ int launchTrace(sail_ctx* c, const SailSample* hs, int count, int maxBounces) {
   // more runs one workgroup per block (no stage).
   const long long stageStride = (long long)owned * 4096;
   const int stageSpp = (int)std::max<long long>(1, (long long)(kStageCapBytes / ((size_t)stageStride * 12)));
-  for (int s0 = 0; s0 < count; s0 += c->launchSpp) {
-    const int nspp = (count - s0) < c->launchSpp ? (count - s0) : c->launchSpp;
+  const int L = launchSamples(c);
+  for (int s0 = 0; s0 < count; s0 += L) {
+    const int nspp = (count - s0) < L ? (count - s0) : L;
     SailTraceArgs A;
     memset(&A, 0, sizeof A);
     A.prims = c->prims; A.typeMasks = reinterpret_cast<const unsigned long long*>(c->prims + c->n);
@@ -1394,7 +1406,7 @@ int sail_set_partition(sail_ctx* c, int rank, int world, int mode) {
 
 int sail_set_launch_samples(sail_ctx* c, int spp) {
   if (!c) return SAIL_E_INVALID;
-  if (spp < 1 || spp > 1 << 20) return fail(c, SAIL_E_INVALID, "launch samples %d", spp);
+  if (spp < 0 || spp > 1 << 20) return fail(c, SAIL_E_INVALID, "launch samples %d", spp);  // 0: by form
   for (sail_ctx* s : c->subs) if (int rc = sail_set_launch_samples(s, spp)) return relay(c, rc, s);
   if (int rc = flushQueued(c)) return rc;
   c->launchSpp = spp;
@@ -1467,7 +1479,7 @@ int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed
   }
   c->k++;
   c->reduced = false;
-  if ((int)c->queued.size() >= c->launchSpp) return flushQueued(c);
+  if ((int)c->queued.size() >= launchSamples(c)) return flushQueued(c);
   return SAIL_OK;
 }
 

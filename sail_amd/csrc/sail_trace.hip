@@ -1836,7 +1836,14 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
   constexpr bool kHome = FAM && !CULL;
   const bool home = !grouped || (kHome && tw.kBeg == 0);
   const bool pixLane = li < kPX;  // the lane that adds its pixel's samples (every lane when NS == 1)
+  // the pixel's running accumulator: in registers, or, with samples in flight (flat forms), in an LDS slot of its lane
+  // (the Cornell form: 32 float4, 512 B; the room form measured more spills with it), so that no VGPR stays live across the sample loop for it
+  constexpr bool kAccLds = NS >= 16 && !CULL;
+  __shared__ float4 sAcc[kAccLds ? kPX : 1];
   float4 acc = (valid && home && pixLane) ? A.accum[pixG] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if constexpr (kAccLds) {
+    if (pixLane) sAcc[li] = acc;  // read back only by this lane
+  }
   const float s = ((float)x + 0.5f) / (float)A.W, t = ((float)y + 0.5f) / (float)A.H;
   const bool tri0 = s + t <= 1.0f;
   const V3 eye = v3(A.eye[0], A.eye[1], A.eye[2]);
@@ -2082,16 +2089,21 @@ __device__ __forceinline__ void traceTileCompact(const SailTraceArgs& A) {
       }
     } else {
       if (valid && pixLane) {  // the pixel's samples of this step, in sample order
+        if constexpr (kAccLds) acc = sAcc[li];
         for (int j = 0; j < NS && k + j < tw.kEnd; j++) {
           const V3 er = E_LOAD(j * kPX + li);
           if (!home) stageSample<kPX>(A, k + j, tw.bid, li, er);
           else accumulateSample(acc, er, constRow<SailSample>(A.samples, k + j), A.accumMode);
         }
+        if constexpr (kAccLds) sAcc[li] = acc;
       }
       if (li < NS && k + NS + li < tw.kEnd) sSeed[li] = constRow<SailSample>(A.samples, k + NS + li).seed;
     }
     __syncthreads();
     PHASE_MARK(pc, 11);  // sample end: barriers, accumulation / staging
+  }
+  if constexpr (kAccLds) {
+    if (pixLane) acc = sAcc[li];
   }
   if (valid && home && pixLane) A.accum[pixG] = acc;
 #if SAIL_PHASE_TIMING

@@ -880,6 +880,31 @@ def test_kernel_build_identity(gpu, fixtures):
     assert n0.startswith("sail_trace_kernel_cornell") and b0 != b1 and j0 == "0" * 16
 
 
+def test_launch_samples_by_form(gpu, fixtures):
+    """samples per launch default to the kernel form's (sail_set_launch_samples 0): the Cornell form with 16 samples in
+    flight runs up to 1,024 per launch, a rank of 8 (1 in flight) and an explicit setting 64; the frame is the same bit
+    for bit however the samples are split into launches"""
+    sc = fixtures["scenes"]["C1"]
+    W, H, B, spp = 1920, 1080, 3, 96
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    out = {}
+    for label, launch, world in (("auto", None, 1), ("fixed", 64, 1), ("rank8", None, 8)):
+        ctx = capi.Context(W, H)
+        try:
+            ctx.set_scene_dict(sc)
+            if launch:
+                ctx.set_launch_samples(launch)
+            ctx.set_partition(0, world)
+            ctx.render_schedule(inv, seeds, sc["eye"], B)
+            out[label] = (ctx.read_accum(), ctx.stats().launches)
+        finally:
+            ctx.close()
+    assert out["auto"][1] == 1 and out["fixed"][1] == 2 and out["rank8"][1] == 2, {k: v[1] for k, v in out.items()}
+    assert bit_equal(out["auto"][0], out["fixed"][0]).all()
+    mask = out["rank8"][0][..., 3] > 0  # rank 0's tiles
+    assert mask.any() and bit_equal(out["rank8"][0][mask], out["auto"][0][mask]).all()
+
+
 def test_cornell_form_follows_the_share_of_the_frame(gpu, fixtures):
     """the Cornell form holds 16 samples in flight for a large share of the frame and 1 for a rank of 8 (sail_capi.cpp
     jitNsFor): set_partition switches the run-time kernel, and back (both are in the cache shipped with the library)"""

@@ -47,6 +47,12 @@ for step in "$@"; do
     sched)  # the run-time kernels under other LLVM machine-scheduler strategies (studies sched_*)
       for sc in C1 C3; do vb sched_$sc 500 $sc cur=main ilp=$V/libsail_hip_sched_ilp.so memclause=$V/libsail_hip_sched_memclause.so iterilp=$V/libsail_hip_sched_iterilp.so; done
       VARIANT_SPP=64 vb sched_C4 700 C4 cur=main ilp=$V/libsail_hip_sched_ilp.so memclause=$V/libsail_hip_sched_memclause.so iterilp=$V/libsail_hip_sched_iterilp.so ;;
+    acclds)  # the Cornell form's running accumulator in LDS (working tree) against the HEAD build
+      vb acclds_C1 400 C1 cur=main head=$V/libsail_hip_head.so
+      vb acclds_C1b 400 C1 cur=main head=$V/libsail_hip_head.so ;;
+    launch)  # samples per launch at 1,024 spp (working tree): fewer, longer-lived waves per frame
+      for L in 64 128 256 1024; do VARIANT_SPP=1024 VARIANT_LAUNCH=$L vb launch_C1_$L 400 C1 cur=main; done
+      for L in 64 256; do VARIANT_SPP=256 VARIANT_LAUNCH=$L vb launch_C3_$L 400 C3 cur=main; done ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done

@@ -7,7 +7,8 @@
 #   bench            bench.py C2 with the CPU baselines               bench_quick bench.py C2, no CPU baseline
 #   bench_c3|c4|c5   the config's full frame                          bench_rccl  C2 through the forced-RCCL branch
 #   prof_c2|c3|c4|c5 rocprofv3 --kernel-trace --stats of the config's bench (C4 at 64 spp: one launch)
-#   pmc_c2|c3|c4|c5  the four PMC passes of tools/pmc.sh, summarised into gpurun_out/summ/$TAG_pmc_summary_<cfg>.json
+#   pmc_c2|c3|c4|c5  the four PMC passes of tools/pmc.sh over one launch of the bench's shape, summarised into
+#                    gpurun_out/summ/$TAG_pmc_summary_<cfg>.json
 #   mix_c2|c3        the VALU instruction-mix passes of tools/pmc_mix.sh, summarised the same way
 #   scale            the per-rank emulation of N = 1/2/4/8 (tools/scaling_probe.py) for C2..C5
 #   variants         tools/variant_bench.py over sail_amd/lib/variants/*.so (VARIANT_ARGS: scene W H B spp ...)
@@ -24,6 +25,8 @@ declare -A PX=([c2]=2073600 [c3]=2073600 [c4]=8294400 [c5]=2073600)
 declare -A BO=([c2]=8 [c3]=8 [c4]=12 [c5]=16)
 declare -A WL=([c2]=cornell_box_readme_C2 [c3]=materials_demo_C3 [c4]=random64_C4 [c5]=cornell_box_converged_C5)
 declare -A OPS=([c2]=298.98 [c3]=889.32 [c4]=4061.12 [c5]=296.66)
+# samples of the one profiled launch: the bench's own launch shape (the Cornell form runs 1,024 samples per launch)
+declare -A LS=([c2]=1024 [c3]=64 [c4]=64 [c5]=1024)
 prof() {  # rocprofv3 kernel stats of a bench run: prof <name> <bench args...>
   local name=$1; shift
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/$name -o run \
@@ -57,12 +60,12 @@ for step in "$@"; do
     prof_c5) prof prof_c5 --config C5 --steps 1 --warmup 1 --no-cpu-baseline || exit 6 ;;
     pmc_c2|pmc_c3|pmc_c4|pmc_c5)
       c=${step#pmc_}; cfg=$(echo $c | tr a-z A-Z)
-      PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=64 bash tools/pmc.sh > /dev/null || exit 7  # one 64-spp launch
-      python tools/pmc_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_summary_$c.json ${PX[$c]} 64 ${BO[$c]} ${WL[$c]} > /dev/null || exit 7 ;;
+      PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=${LS[$c]} bash tools/pmc.sh > /dev/null || exit 7  # one launch
+      python tools/pmc_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_summary_$c.json ${PX[$c]} ${LS[$c]} ${BO[$c]} ${WL[$c]} > /dev/null || exit 7 ;;
     mix_c2|mix_c3)
       c=${step#mix_}; cfg=$(echo $c | tr a-z A-Z)
-      PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=64 bash tools/pmc_mix.sh > /dev/null || exit 8
-      python tools/pmc_mix_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_valu_mix_$c.json ${PX[$c]} 64 ${BO[$c]} ${WL[$c]} ${OPS[$c]} > /dev/null || exit 8 ;;
+      PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=${LS[$c]} bash tools/pmc_mix.sh > /dev/null || exit 8
+      python tools/pmc_mix_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_valu_mix_$c.json ${PX[$c]} ${LS[$c]} ${BO[$c]} ${WL[$c]} ${OPS[$c]} > /dev/null || exit 8 ;;
     scale)
       for a in "C2 1024" "C3 256" "C4 32" "C5 1024"; do
         timeout -k 10 300 python -u tools/scaling_probe.py $a >> $OUT/scale.jsonl 2>&1 || exit 9
