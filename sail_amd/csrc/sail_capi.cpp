@@ -1479,7 +1479,10 @@ int sail_render(sail_ctx* c, const float inv[16], const float eye[3], float seed
   }
   c->k++;
   c->reduced = false;
-  if ((int)c->queued.size() >= launchSamples(c)) return flushQueued(c);
+  // one-sample frames launch 64 at a time unless the host fixed the launch size: the host keeps queueing the next
+  // frames while a launch runs (a whole 1,024-frame queue launched at once left the GPU idle meanwhile: the JS host's
+  // render() per frame at 85,391 against 91,161 Msamples/s, profiles/r05_bench_js_host*.json)
+  if ((int)c->queued.size() >= (c->launchSpp > 0 ? c->launchSpp : 64)) return flushQueued(c);
   return SAIL_OK;
 }
 
