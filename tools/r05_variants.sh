@@ -53,6 +53,8 @@ for step in "$@"; do
     launch)  # samples per launch at 1,024 spp (working tree): fewer, longer-lived waves per frame
       for L in 64 128 256 1024; do VARIANT_SPP=1024 VARIANT_LAUNCH=$L vb launch_C1_$L 400 C1 cur=main; done
       for L in 64 256; do VARIANT_SPP=256 VARIANT_LAUNCH=$L vb launch_C3_$L 400 C3 cur=main; done ;;
+    acclds_room)  # the room form's running accumulator in LDS (study acclds_room)
+      for sc in C3 UI; do vb acclds_room_$sc 400 $sc cur=main room=$V/libsail_hip_acclds_room.so; done ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
