@@ -205,9 +205,9 @@ int sail_jit_compile(const sail_plugins* plugins, int mode, const int32_t* row_t
  * tracer.js:42-90 -> webgl.js:165-192); a hipRTC compile takes seconds, so sail_set_scene / sail_update_objects only
  * START the build of the scene's run-time kernel, on a background thread, and return; launches use the precompiled
  * kernel of the scene's plugin set until the module is loaded (bit-identical frames). Code objects are cached on disk,
- * keyed by (arch, spec, kernel-source hash, compile flags, hipRTC version): a read-only cache beside the library
- * (<lib dir>/jit, filled by sail_jit_prebuild at build time) and the user's cache. A hipRTC whose version differs from
- * the library's build is refused (the precompiled kernels serve). */
+ * keyed by (arch, spec, kernel-source hash, compile flags, compiler version): a read-only cache beside the library
+ * (<lib dir>/jit, filled by sail_jit_prebuild at build time) and the user's cache. A code object produced by another
+ * compiler than the one that built the library is refused (the precompiled kernels serve). */
 enum sail_kernel_jit_state {
   SAIL_KERNEL_JIT_NONE = 0,     /* the scene gets no run-time kernel (switches, or a precompiled kernel is exact) */
   SAIL_KERNEL_JIT_PENDING = 1,  /* being built in the background */
