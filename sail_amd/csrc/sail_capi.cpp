@@ -16,7 +16,6 @@
 
 // launch wrappers defined next to the kernels (sail_trace.hip)
 hipError_t sail_launch_trace(const SailTraceArgs& A, int blocks, hipStream_t s);
-extern const int sail_trace_phase_timing;  // sail_trace.hip: 1 in the phase-timing build (libsail_hip_phase.so)
 // sail_jit.cpp: the trace kernel pair compiled at run time for exactly one plugin set (on the current device)
 #include "sail_jit.h"
 hipError_t sail_launch_filter(const SailFilterArgs& A, hipStream_t s);
@@ -145,7 +144,7 @@ struct sail_ctx {
   int forceGeneric = 0;  // SAIL_FORCE_GENERIC=1: always launch the all-plugin kernel (tests)
   int forceGroups = 0;   // SAIL_SAMPLE_GROUPS=g: fixed sample-group count (tests); 0 = by occupancy
   int wavefront = 0;     // SAIL_DEBUG_WAVEFRONT: the pre-cull path by the wavefront split (study)
-  int jit = sail_trace_phase_timing ? 0 : 27;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels)
+  int jit = 27;  // SAIL_DEBUG_JIT bits: which scenes get a run-time kernel (jitKernels; instrumented in the phase build)
   // The scene's run-time kernel (refreshJit): its spec, and whether it is still being built, loaded or failed. Until it
   // is loaded the precompiled kernel of the scene's set serves (same results); a launch waits up to jitWait ms for it
   // (SAIL_DEBUG_JIT_WAIT; -1 until it is built).

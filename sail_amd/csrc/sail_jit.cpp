@@ -47,6 +47,7 @@
 extern const char* const sail_jit_src_names[];
 extern const char* const sail_jit_src_texts[];
 extern const int sail_jit_src_count;
+extern const int sail_trace_phase_timing;  // sail_trace.hip: 1 in the phase-timing build (libsail_hip_phase.so)
 
 int sailJitThreads(const SailJitSpec& s) { return s.nt ? s.nt : (s.mode == 1 ? 1024 : 256); }
 bool sailJitSpecEqual(const SailJitSpec& a, const SailJitSpec& b) {
@@ -106,7 +107,8 @@ std::string defsFor(const SailJitSpec& sp) {
            "#define SAIL_JIT_TN %d\n#define SAIL_JIT_NS %d\n#include \"sail_trace.hip\"\n",
            sp.waves, sp.mode == 1, sp.mode == 2, sp.ks, sp.km, sp.kt, sp.kl, sailJitThreads(sp), sp.rows,
            sp.rows ? types.c_str() : "0", sp.ldsFit, sp.tn, sp.ns);
-  return defs;
+  // the phase-timing build compiles its run-time kernels instrumented as well (their own g_sailPhase)
+  return sail_trace_phase_timing ? std::string("#define SAIL_PHASE_TIMING 1\n") + defs : std::string(defs);
 }
 
 // hipRTC entry points from the toolchain's library (SAIL_HIPRTC, else $ROCM_PATH or /opt/rocm, lib/libhiprtc.so.7)
@@ -565,4 +567,21 @@ uint64_t sail_precompiled_build_id(const char* kernel) {
     return h;
   }();
   return fnvStr(kernel, lib);
+}
+
+// The phase-timing build: the per-phase sums of every loaded run-time module, added to out (reset: zeroed)
+int sail_jit_phase_read(unsigned long long out[12], int reset) {
+  std::lock_guard<std::mutex> lk(g_loadMutex);
+  for (auto& kv : g_loaded) {
+    hipDeviceptr_t p = nullptr;
+    size_t bytes = 0;
+    if (hipSetDevice(kv.first.first) != hipSuccess) return -1;
+    if (hipModuleGetGlobal(&p, &bytes, kv.second.mod, "g_sailPhase") != hipSuccess || bytes < 12 * sizeof(unsigned long long))
+      continue;  // a module compiled before the switch (not instrumented)
+    unsigned long long v[12];
+    if (hipMemcpyDtoH(v, p, sizeof v) != hipSuccess) return -1;
+    for (int q = 0; q < 12; q++) out[q] += v[q];
+    if (reset && hipMemsetD8(p, 0, sizeof v) != hipSuccess) return -1;
+  }
+  return 0;
 }

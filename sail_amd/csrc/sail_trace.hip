@@ -37,6 +37,13 @@ using namespace sm;
 
 #define D __device__ __forceinline__
 
+#if defined(SAIL_PHASE_TIMING) && SAIL_PHASE_TIMING
+// the phase-timing build's per-phase wave-cycle sums: C linkage, so that a run-time compiled module's own copy can be
+// found by name (sail_jit_phase_read)
+extern "C" __device__ unsigned long long g_sailPhase[12];
+__device__ unsigned long long g_sailPhase[12];
+#endif
+
 namespace {
 
 constexpr float kMaxDistance = 1e5f, kEps = 1e-5f, kOneMinusEps = 0.9999f, kInf = 1e5f;
@@ -141,7 +148,6 @@ D Ray mkRay(V3 o, V3 d) {
 #define SAIL_PHASE_TIMING 0
 #endif
 #if SAIL_PHASE_TIMING
-__device__ unsigned long long g_sailPhase[12];
 struct PhaseClock { unsigned long long t, acc[12]; };
 #define PHASE_MARK(pc, k) do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); (pc).acc[k] += now_ - (pc).t; (pc).t = now_; } while (0)
 #else
@@ -2576,17 +2582,18 @@ extern "C" __global__ void sail_math_kernel(int fn, const float* x, const float*
   out[i] = r;
 }
 
-// the phase-timing build's contexts keep to these (instrumented) kernels: no run-time compiled ones (sail_capi.cpp)
+// 1 in the phase-timing build: its run-time kernels are compiled instrumented too (sail_jit.cpp defsFor)
 extern const int sail_trace_phase_timing = SAIL_PHASE_TIMING;
 #if SAIL_PHASE_TIMING
-// phase-timing readout for the variant harness (tools/variant_bench.py --phases)
+int sail_jit_phase_read(unsigned long long out[12], int reset);  // sail_jit.cpp: the loaded run-time modules' sums
+// phase-timing readout (tools/phase_profile.py): the precompiled kernels' sums plus every loaded run-time module's
 extern "C" int sail_phase_read(unsigned long long out[12], int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sailPhase), 12 * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
     const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_sailPhase), z, sizeof z) != hipSuccess) return -1;
   }
-  return 0;
+  return sail_jit_phase_read(out, reset);
 }
 #endif
 

@@ -614,7 +614,8 @@ def test_last_bounce_shortcut_edge_materials(gpu, fixtures, variant, B):
 @pytest.mark.parametrize("name,W,H,spp,B", [("C1", 40, 24, 3, 6), ("C3", 40, 24, 3, 5), ("C4", 40, 24, 2, 6)])
 def test_phase_timing_build_bit_exact(gpu, fixtures, monkeypatch, name, W, H, spp, B):
     """libsail_hip_phase.so (-DSAIL_PHASE_TIMING=1, tools/phase_profile.py) renders the oracle's bits in all three
-    kernel families and its per-phase wave timers advance"""
+    kernel families, through run-time kernels compiled instrumented as well, and its per-phase wave timers advance
+    (summed over the library's kernels and the loaded run-time modules)"""
     import ctypes
     import os
     path = os.path.join(os.path.dirname(capi.LIB_PATH), "libsail_hip_phase.so")
@@ -632,10 +633,12 @@ def test_phase_timing_build_bit_exact(gpu, fixtures, monkeypatch, name, W, H, sp
         ctx.set_scene_dict(sc)
         ctx.render_schedule(inv, seeds, sc["eye"], B)
         got = ctx.read_accum()
+        kname = ctx.kernel_name()
     finally:
         ctx.close()
     want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B)
     assert bit_equal(got, want).all()
+    assert "_jit" in kname, kname
     assert lib.sail_phase_read(buf, 0) == 0
     assert buf[0] > 0 and buf[1] > 0  # sweep and hit-record phases were timed
 
