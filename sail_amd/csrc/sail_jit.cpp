@@ -572,16 +572,20 @@ uint64_t sail_precompiled_build_id(const char* kernel) {
 // The phase-timing build: the per-phase sums of every loaded run-time module, added to out (reset: zeroed)
 int sail_jit_phase_read(unsigned long long out[12], int reset) {
   std::lock_guard<std::mutex> lk(g_loadMutex);
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return -1;
+  int rc = 0;
   for (auto& kv : g_loaded) {
     hipDeviceptr_t p = nullptr;
     size_t bytes = 0;
-    if (hipSetDevice(kv.first.first) != hipSuccess) return -1;
+    if (hipSetDevice(kv.first.first) != hipSuccess) { rc = -1; break; }
     if (hipModuleGetGlobal(&p, &bytes, kv.second.mod, "g_sailPhase") != hipSuccess || bytes < 12 * sizeof(unsigned long long))
-      continue;  // a module compiled before the switch (not instrumented)
+      continue;  // not instrumented
     unsigned long long v[12];
-    if (hipMemcpyDtoH(v, p, sizeof v) != hipSuccess) return -1;
+    if (hipMemcpyDtoH(v, p, sizeof v) != hipSuccess) { rc = -1; break; }
     for (int q = 0; q < 12; q++) out[q] += v[q];
-    if (reset && hipMemsetD8(p, 0, sizeof v) != hipSuccess) return -1;
+    if (reset && hipMemsetD8(p, 0, sizeof v) != hipSuccess) { rc = -1; break; }
   }
-  return 0;
+  (void)hipSetDevice(cur);  // the caller's current device
+  return rc;
 }
