@@ -216,8 +216,9 @@ enum sail_kernel_jit_state {
 };
 typedef struct sail_kernel_info {
   char name[64];          /* the kernel the last launch ran (sail_kernel_name) */
-  uint64_t build_id;      /* its build identity: FNV-1a 64 of the code object (run-time kernels) or of the library
-                           * image and the kernel's name (precompiled): profiles are matched to kernels by it */
+  uint64_t build_id;      /* its build identity: FNV-1a 64 of the code object with the compiler's source-derived
+                           * compilation-unit id masked (run-time kernels), or of the library image and the kernel's name
+                           * (precompiled): profiles are matched to kernels by it */
   int jit_state;          /* sail_kernel_jit_state of the scene's run-time kernel */
   int jit_from_cache;     /* its code object came from 0: hipRTC in this process, 1: the user's disk cache, 2: the
                            * cache shipped beside the library */

@@ -20,6 +20,7 @@
 // the same sonames -- would otherwise compile with that one, and the kernels would differ from the precompiled ones
 // (tests/test_jit_compile.py checks instruction identity after importing torch). A code object produced by another
 // compiler than the one this library was built with is refused (sameCompiler; the precompiled kernels serve).
+#include <ctype.h>
 #include <dlfcn.h>
 #include <pthread.h>
 #include <errno.h>
@@ -317,11 +318,23 @@ struct Entry {
 std::mutex g_mapMutex;
 std::map<std::pair<std::string, Key>, std::shared_ptr<Entry>> g_code;
 
+// The build identity of a code object: FNV-1a 64 of its bytes with the compilation-unit id the compiler derives from
+// the source text (the `__hip_cuid_<hex>` symbol name) masked, so that an edit that changes no instruction (a comment)
+// keeps the id, and any change to code, data or metadata changes it.
+uint64_t codeId(const std::vector<char>& code) {
+  std::vector<char> c(code);
+  static const char tag[] = "__hip_cuid_";
+  for (auto it = c.begin(); (it = std::search(it, c.end(), tag, tag + sizeof tag - 1)) != c.end();) {
+    it += sizeof tag - 1;
+    for (; it != c.end() && isxdigit((unsigned char)*it); ++it) *it = '0';
+  }
+  return fnv(c.data(), c.size());
+}
 void finish(Entry& e, std::vector<char>& code, const std::string& err, double ms, int from) {
   {
     std::lock_guard<std::mutex> lk(e.m);
     if (!code.empty()) {
-      e.id = fnv(code.data(), code.size());
+      e.id = codeId(code);
       e.code.swap(code);
       e.compileMs = ms;
       e.fromCache = from;

@@ -23,7 +23,7 @@ int sailJitThreads(const SailJitSpec& s);  // threads per workgroup of the spec'
 // A loaded kernel pair and where its code object came from.
 struct SailJitKernel {
   hipFunction_t plain = nullptr, grouped = nullptr;
-  uint64_t buildId = 0;     // FNV-1a 64 of the code object (the kernel's build identity)
+  uint64_t buildId = 0;     // FNV-1a 64 of the code object, its compilation-unit id masked (sail_jit.cpp codeId)
   double compileMs = 0.0;   // hipRTC time of the code object (0 when it came from a disk cache)
   int fromCache = 0;        // 1: the user's on-disk cache, 2: the cache shipped next to the library
 };
