@@ -55,6 +55,8 @@ for step in "$@"; do
       for L in 64 256; do VARIANT_SPP=256 VARIANT_LAUNCH=$L vb launch_C3_$L 400 C3 cur=main; done ;;
     acclds_room)  # the room form's running accumulator in LDS (study acclds_room)
       for sc in C3 UI; do vb acclds_room_$sc 400 $sc cur=main room=$V/libsail_hip_acclds_room.so; done ;;
+    twobar2)  # the Cornell form's two-barrier sort re-measured at whole-frame launches (study cornell_twobar)
+      VARIANT_SPP=1024 VARIANT_LAUNCH=1024 vb twobar2_C1 500 C1 cur=main twobar=$V/libsail_hip_cornell_twobar.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
