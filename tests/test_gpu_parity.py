@@ -908,6 +908,30 @@ def test_launch_samples_by_form(gpu, fixtures):
     assert mask.any() and bit_equal(out["rank8"][0][mask], out["auto"][0][mask]).all()
 
 
+@pytest.mark.parametrize("mode", [capi.ACCUM_SUM, capi.ACCUM_MIX, capi.ACCUM_COMPAT8])
+def test_whole_frame_launches_cross_a_launch_boundary(gpu, fixtures, mode):
+    """the Cornell form with 16 samples in flight launches up to 1,024 samples at once: 1,100 samples run as 1,024 + 76,
+    each pixel's running accumulator kept in LDS across the 64 + 5 sample steps, bit-exact against the oracle in every
+    accumulation mode; and sail_set_launch_samples(0) returns a fixed launch size to the form's"""
+    sc = fixtures["scenes"]["C1"]
+    W, H, B, spp = 24, 16, 3, 1100
+    inv, seeds = capi.schedule(np.array(sc["mvp_rowmajor"]), W, H, 0, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), W, H, inv, seeds, sc["eye"], B, accum_mode=mode)
+    ctx = capi.Context(W, H, debug={capi.DEBUG_JIT_NS: 16})
+    try:
+        ctx.set_accum_mode(mode)
+        ctx.set_scene_dict(sc)
+        ctx.set_launch_samples(64)
+        ctx.set_launch_samples(0)
+        ctx.render_schedule(inv, seeds, sc["eye"], B)
+        got = ctx.read_accum()
+        st = ctx.stats()
+    finally:
+        ctx.close()
+    assert st.launches == 2
+    assert bit_equal(got, want).all()
+
+
 def test_cornell_form_follows_the_share_of_the_frame(gpu, fixtures):
     """the Cornell form holds 16 samples in flight for a large share of the frame and 1 for a rank of 8 (sail_capi.cpp
     jitNsFor): set_partition switches the run-time kernel, and back (both are in the cache shipped with the library)"""
