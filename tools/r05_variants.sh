@@ -57,6 +57,8 @@ for step in "$@"; do
       for sc in C3 UI; do vb acclds_room_$sc 400 $sc cur=main room=$V/libsail_hip_acclds_room.so; done ;;
     twobar2)  # the Cornell form's two-barrier sort re-measured at whole-frame launches (study cornell_twobar)
       VARIANT_SPP=1024 VARIANT_LAUNCH=1024 vb twobar2_C1 500 C1 cur=main twobar=$V/libsail_hip_cornell_twobar.so ;;
+    roomwaves)  # the room form's occupancy with 4 samples in flight (studies room_w8, room_w6)
+      vb roomwaves_C3 500 C3 cur=main w8=$V/libsail_hip_room_w8.so w6=$V/libsail_hip_room_w6.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
