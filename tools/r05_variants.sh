@@ -59,6 +59,8 @@ for step in "$@"; do
       VARIANT_SPP=1024 VARIANT_LAUNCH=1024 vb twobar2_C1 500 C1 cur=main twobar=$V/libsail_hip_cornell_twobar.so ;;
     roomwaves)  # the room form's occupancy with 4 samples in flight (studies room_w8, room_w6)
       vb roomwaves_C3 500 C3 cur=main w8=$V/libsail_hip_room_w8.so w6=$V/libsail_hip_room_w6.so ;;
+    sorthalf)  # the Cornell form sorting every other bounce (studies cornell_sort_even / _odd)
+      VARIANT_SPP=1024 VARIANT_LAUNCH=1024 vb sorthalf_C1 500 C1 cur=main even=$V/libsail_hip_cornell_sort_even.so odd=$V/libsail_hip_cornell_sort_odd.so ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
