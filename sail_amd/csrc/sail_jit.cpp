@@ -30,6 +30,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <algorithm>
@@ -318,17 +319,35 @@ struct Entry {
 std::mutex g_mapMutex;
 std::map<std::pair<std::string, Key>, std::shared_ptr<Entry>> g_code;
 
-// The build identity of a code object: FNV-1a 64 of its bytes with the compilation-unit id the compiler derives from
-// the source text (the `__hip_cuid_<hex>` symbol name) masked, so that an edit that changes no instruction (a comment)
-// keeps the id, and any change to code, data or metadata changes it.
+// The build identity of a code object: FNV-1a 64 over the sections that hold what runs -- the instructions (.text), the
+// kernel descriptors (.rodata), the code-object metadata (.note: registers, LDS, launch bounds) and any initialised
+// data -- each with its name. The symbol, string and hash tables are left out: they carry the compilation-unit id the
+// compiler derives from the source text (`__hip_cuid_<hex>`), so an edit that changes no instruction (a comment, code
+// compiled out of this kernel) keeps the id, and any change to what runs changes it. Not an ELF: the whole image.
 uint64_t codeId(const std::vector<char>& code) {
-  std::vector<char> c(code);
-  static const char tag[] = "__hip_cuid_";
-  for (auto it = c.begin(); (it = std::search(it, c.end(), tag, tag + sizeof tag - 1)) != c.end();) {
-    it += sizeof tag - 1;
-    for (; it != c.end() && isxdigit((unsigned char)*it); ++it) *it = '0';
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(code.data());
+  const size_t n = code.size();
+  auto u16 = [&](size_t o) { return o + 2 <= n ? (uint64_t)b[o] | (uint64_t)b[o + 1] << 8 : 0; };
+  auto u32 = [&](size_t o) { return o + 4 <= n ? u16(o) | u16(o + 2) << 16 : 0; };
+  auto u64 = [&](size_t o) { return o + 8 <= n ? u32(o) | u32(o + 4) << 32 : 0; };
+  if (n < 64 || memcmp(b, "\177ELF", 4) != 0 || b[4] != 2) return fnv(code.data(), n);  // ELF64 only
+  const uint64_t shoff = u64(0x28), shentsize = u16(0x3a), shnum = u16(0x3c), shstrndx = u16(0x3e);
+  if (shentsize < 64 || shstrndx >= shnum || shoff + shnum * shentsize > n) return fnv(code.data(), n);
+  const uint64_t strOff = u64(shoff + shstrndx * shentsize + 0x18), strSize = u64(shoff + shstrndx * shentsize + 0x20);
+  if (strOff + strSize > n) return fnv(code.data(), n);
+  uint64_t h = fnv("sail-code", 9);
+  for (uint64_t k = 0; k < shnum; k++) {
+    const size_t e = shoff + k * shentsize;
+    const uint64_t nameOff = u32(e), type = u32(e + 4), off = u64(e + 0x18), size = u64(e + 0x20);
+    if (nameOff >= strSize) continue;
+    const char* name = reinterpret_cast<const char*>(b + strOff + nameOff);
+    const size_t nameLen = strnlen(name, strSize - nameOff);
+    const std::string nm(name, nameLen);
+    if (nm != ".text" && nm != ".rodata" && nm != ".note" && nm != ".data") continue;
+    h = fnvStr(nm, h);
+    if (type != 8 /* SHT_NOBITS */ && off + size <= n) h = fnv(b + off, size, h);
   }
-  return fnv(c.data(), c.size());
+  return h;
 }
 void finish(Entry& e, std::vector<char>& code, const std::string& err, double ms, int from) {
   {
