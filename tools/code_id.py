@@ -1,3 +1,6 @@
+#!/usr/bin/env python3
+"""The build identity of run-time code objects as sail_jit.cpp codeId computes it: FNV-1a 64 over the .text, .rodata,
+.note and .data sections (with their names). Usage: tools/code_id.py FILE.co ... (SAILJIT1 cache files or bare ELF)."""
 import struct, sys
 def fnv(b, h=14695981039346656037):
     for x in b:
