@@ -61,6 +61,8 @@ for step in "$@"; do
       vb roomwaves_C3 500 C3 cur=main w8=$V/libsail_hip_room_w8.so w6=$V/libsail_hip_room_w6.so ;;
     sorthalf)  # the Cornell form sorting every other bounce (studies cornell_sort_even / _odd)
       VARIANT_SPP=1024 VARIANT_LAUNCH=1024 vb sorthalf_C1 500 C1 cur=main even=$V/libsail_hip_cornell_sort_even.so odd=$V/libsail_hip_cornell_sort_odd.so ;;
+    boxface)  # the room form's first box row (Cube too) sorted by face (study room_box_face_key)
+      for sc in C3 UI AREA; do vb boxface_$sc 400 $sc cur=main box=$V/libsail_hip_room_box_face_key.so; done ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
