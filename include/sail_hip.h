@@ -274,6 +274,31 @@ int sail_accum_device_ptr(sail_ctx* ctx, void** ptr, size_t* bytes);
 /* the 64x64 tiles rank `rank` of `world` owns in a W x H frame (tile t -> rank t % world), as
  * (x0, y0, w, h) quadruples; returns the tile count (or a negative error); out may be NULL to count */
 int sail_partition_tiles(int width, int height, int rank, int world, int* out_xywh, int capacity);
+/* Host only (no device): the bookkeeping both reduces follow -- sail_reduce (one process per GPU) and a multi-device
+ * context's grouped reduce -- for rank `rank` of `world` under partition `mode` once k samples (global indices
+ * 0 .. k-1) are rendered, the frame reduced into `root`. Both derive their choices from this function, so a host
+ * language, or a test over gloo (tests/test_partition_gloo.py), plans the same exchange without a device. */
+typedef struct sail_reduce_plan {
+  int receives;       /* 1: this rank is `root`, where the reduced frame lands */
+  int tiles;          /* 64x64 tiles this rank renders: tiles t = rank (mod world), or every tile (sample partition) */
+  int aov_owner;      /* the rank whose AOV maps the frame shows: the one that rendered sample k-1 (sample partition; 0
+                       * before any sample), or -1 for a tile partition (every rank owns its own tiles' maps) */
+  int send_own_aovs;  /* 1: this rank reduces its own AOV maps; 0: it sends -0 maps, the additive identity that keeps
+                       * every bit of the owner's maps (x + -0 == x for +-0 and NaN too) */
+  uint64_t samples;   /* how many of the samples 0 .. k-1 this rank rendered: k for a tile partition, those with index
+                       * = rank (mod world) for a sample partition */
+} sail_reduce_plan;
+int sail_plan_reduce(int width, int height, int rank, int world, int mode, uint64_t k, int root, sail_reduce_plan* out);
+/* Host only: what rank `rank` keeps of a whole-frame accumulator when it resumes from it (sail_load_accum part -1):
+ * its own tiles and zeros elsewhere, or for a sample partition all of it on rank 0 and zeros on the others. sums and
+ * out hold W*H*4 floats (they may be the same buffer). */
+int sail_plan_keep(int width, int height, int rank, int world, int mode, const float* sums, float* out);
+/* Host only: one step of a part-wise checkpoint load over `parts` parts (sail_load_accum on a multi-device context).
+ * *missing = bit mask of the parts still to load (0: no load in progress), *k = the checkpoint's sample index. Loading
+ * part `part` saved at index k_part: the first part of a checkpoint sets *missing to every part and *k = k_part, then
+ * clears its own bit; a later part with another index fails with SAIL_E_INVALID and leaves the state unchanged; part -1
+ * (a whole frame) clears *missing. A frame is usable again once *missing is 0. */
+int sail_plan_load_part(uint64_t* missing, uint64_t* k, int parts, int part, uint64_t k_part);
 
 /* ---- diagnostics ---- */
 /* evaluate the build's f32 math spec on the device (fn: 0 sin 1 cos 2 tan 3 atan2(y,x) 4 acos 5 pow(x,y)

@@ -46,6 +46,7 @@ EXPORTS = (
     "sail_prim_bounds", "sail_math_probe", "sail_pick", "sail_kernel_name", "sail_filter_ms",
     "sail_abi_version", "sail_accum_parts", "sail_save_accum", "sail_load_accum", "sail_jit_compile",
     "sail_get_kernel_info", "sail_kernel_ready", "sail_set_jit_cache", "sail_jit_prebuild",
+    "sail_plan_reduce", "sail_plan_keep", "sail_plan_load_part",
 )
 
 
@@ -68,6 +69,11 @@ class KernelInfo(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 64), ("build_id", ctypes.c_uint64), ("jit_state", ctypes.c_int),
                 ("jit_from_cache", ctypes.c_int), ("jit_compile_ms", ctypes.c_double), ("jit_build_id", ctypes.c_uint64),
                 ("jit_error", ctypes.c_char * 256)]
+
+
+class ReducePlan(ctypes.Structure):
+    _fields_ = [("receives", ctypes.c_int), ("tiles", ctypes.c_int), ("aov_owner", ctypes.c_int),
+                ("send_own_aovs", ctypes.c_int), ("samples", ctypes.c_uint64)]
 
 
 _SHAPES = {"cube": 1, "sphere": 2, "rectangle": 3, "cone": 4, "cylinder": 5, "disk": 6,
@@ -150,6 +156,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "sail_set_jit_cache": (ctypes.c_int, [ctypes.c_char_p]),
         "sail_jit_prebuild": (ctypes.c_int, [f32p, ctypes.c_int, f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.POINTER(Plugins),
                                              ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+        "sail_plan_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ReducePlan)]),
+        "sail_plan_keep": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p, f32p]),
+        "sail_plan_load_part": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -213,6 +224,50 @@ def partition_tiles(width: int, height: int, rank: int, world: int) -> np.ndarra
     out = np.zeros((max(n, 1), 4), dtype=np.int32)
     lib.sail_partition_tiles(width, height, rank, world, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), n)
     return out[:n]
+
+
+def plan_reduce(width: int, height: int, rank: int, world: int, mode: int, k: int, root: int = 0) -> dict:
+    """The library's reduce bookkeeping for one rank (sail_plan_reduce, host-only): receives, tiles, aov_owner,
+    send_own_aovs, samples."""
+    lib = load()
+    p = ReducePlan()
+    rc = lib.sail_plan_reduce(width, height, rank, world, mode, k, root, ctypes.byref(p))
+    if rc:
+        raise SailError(f"sail_plan_reduce: {rc}: {lib.sail_last_error(None).decode()}")
+    return {f: getattr(p, f) for f, _ in ReducePlan._fields_}
+
+
+def plan_keep(width: int, height: int, rank: int, world: int, mode: int, sums: np.ndarray) -> np.ndarray:
+    """What a rank keeps of a whole-frame accumulator when resuming from it (sail_plan_keep, host-only)."""
+    lib = load()
+    src = _f32(sums).reshape(-1)
+    if src.size != width * height * 4:
+        raise SailError("plan_keep: sums must hold W*H*4 floats")
+    out = np.empty_like(src)
+    rc = lib.sail_plan_keep(width, height, rank, world, mode, _ptr(src), _ptr(out))
+    if rc:
+        raise SailError(f"sail_plan_keep: {rc}")
+    return out.reshape(height, width, 4)
+
+
+class LoadParts:
+    """A part-wise checkpoint load's bookkeeping (sail_plan_load_part, host-only): the parts still missing and the
+    checkpoint's sample index."""
+
+    def __init__(self, parts: int):
+        self.parts = parts
+        self.missing = ctypes.c_uint64(0)
+        self.k = ctypes.c_uint64(0)
+
+    def load(self, part: int, k: int) -> None:
+        lib = load()
+        rc = lib.sail_plan_load_part(ctypes.byref(self.missing), ctypes.byref(self.k), self.parts, part, k)
+        if rc:
+            raise SailError(lib.sail_last_error(None).decode())
+
+    @property
+    def complete(self) -> bool:
+        return self.missing.value == 0
 
 
 def prim_bounds(objects, n: int, tn: int) -> np.ndarray:

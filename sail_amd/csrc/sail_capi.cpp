@@ -332,10 +332,16 @@ bool jitSpecFor(const sail_ctx* c, SailJitSpec* out, int* mode) {
 // Re-derive the scene's run-time kernel after anything it depends on changed (scene, rows, switches). A new spec starts
 // its background build now (Tracer.update links the scene's program, tracer.js:42-90), so the caller never waits for it.
 void refreshJit(sail_ctx* c) {
+  // a multi-device context renders through its sub-contexts, which derive their own kernels (its own plugins and rows
+  // are not kept: a spec derived here would be a useless build)
+  if (!c->subs.empty()) return;
   SailJitSpec spec;
   int mode = 0;
   const bool have = jitSpecFor(c, &spec, &mode);
   if (have == c->jitHave && (!have || sailJitSpecEqual(spec, c->jitSpec))) return;
+  // hold the new spec before dropping the old one: a build both share is never skipped in between
+  if (have) sail_jit_hold(c->device, spec, +1);
+  if (c->jitHave) sail_jit_hold(c->device, c->jitSpec, -1);
   c->jitHave = have;
   c->jitSpec = spec;
   c->jitMode = mode;
@@ -917,9 +923,34 @@ int groupCommCheck(sail_ctx* g) {
   return SAIL_OK;
 }
 
-// The sample-partition rank (device) that rendered the frame's last sample: its AOVs are the frame's, as on one GPU
-// (sample k is rendered by rank k % world; k = the context's sample count)
-int aovOwner(uint64_t k, int world) { return k > 0 ? (int)((k - 1) % (uint64_t)world) : 0; }
+// The reduce plan of rank `rank` of `world` (sail_plan_reduce): the one place sail_reduce and groupReduce take their
+// choices from. A sample partition shows the AOVs of the rank (device) that rendered the frame's last sample, as on one
+// GPU (sample k is rendered by rank k % world; k = the context's sample count); every other rank sends -0 maps.
+sail_reduce_plan planReduce(int W, int H, int rank, int world, int mode, uint64_t k, int root) {
+  sail_reduce_plan p;
+  memset(&p, 0, sizeof p);
+  const bool tiles = mode == SAIL_PART_TILES;
+  const int tx = (W + 63) / 64, ty = (H + 63) / 64, total = tx * ty;
+  p.receives = rank == root;
+  p.tiles = tiles ? (rank < total ? (total - rank + world - 1) / world : 0) : total;
+  p.aov_owner = tiles ? -1 : (k > 0 ? (int)((k - 1) % (uint64_t)world) : 0);
+  p.send_own_aovs = tiles || rank == p.aov_owner;
+  if (tiles || world <= 1) p.samples = k;
+  else p.samples = k > (uint64_t)rank ? (k - 1 - (uint64_t)rank) / (uint64_t)world + 1 : 0;
+  return p;
+}
+// one step of a part-wise checkpoint load (sail_plan_load_part): SAIL_OK or SAIL_E_INVALID, state unchanged on error
+int planLoadPart(uint64_t* missing, uint64_t* k, int parts, int part, uint64_t kPart) {
+  if (parts < 1 || parts > 64 || part < -1 || part >= parts) return SAIL_E_INVALID;
+  if (part == -1) { *missing = 0; *k = kPart; return SAIL_OK; }
+  const uint64_t all = parts >= 64 ? ~0ull : (1ull << parts) - 1ull;
+  uint64_t m = *missing, kk = *k;
+  if (!m) { m = all; kk = kPart; }
+  else if (kPart != kk) return SAIL_E_INVALID;
+  *missing = m & ~(1ull << part);
+  *k = kk;
+  return SAIL_OK;
+}
 // -0 in every component: the additive identity that keeps each AOV bit (x + -0 == x for +-0 and NaN too)
 hipError_t fillNegZero(float4* p, size_t np, hipStream_t s) {
   return hipMemsetD32Async((hipDeviceptr_t)p, (int)0x80000000u, np * 4, s);
@@ -939,7 +970,10 @@ int groupReduce(sail_ctx* g) {
   if (int rc = ensureFrame(r)) return relay(g, rc, r);
   const bool tiles = g->partMode == SAIL_PART_TILES;
   const size_t np = (size_t)g->W * g->H, bytes = np * sizeof(float4);
-  const int owner = aovOwner(r->k, nd);
+  // every device's share of the exchange (sail_plan_reduce: device i = rank i of nd, root 0)
+  std::vector<sail_reduce_plan> plan((size_t)nd);
+  for (int i = 0; i < nd; i++) plan[i] = planReduce(g->W, g->H, i, nd, g->partMode, r->k, 0);
+  const int owner = tiles ? 0 : plan[0].aov_owner;
   if (g->groupLocal) {  // every "device" is the same GPU: wait for the others' streams, sum in rank order
     for (sail_ctx* s : g->subs) HIPCHK(g, hipStreamSynchronize(s->stream));
     auto sum = [&](float4* dst, float4* sail_ctx::*src) -> hipError_t {
@@ -961,7 +995,7 @@ int groupReduce(sail_ctx* g) {
         sail_ctx* s = g->subs[i];
         HIPCHK(g, hipSetDevice(s->device));
         if (int rc = ensureFrame(s)) return relay(g, rc, s);
-        if (i != owner) {
+        if (!plan[i].send_own_aovs) {
           if (s->frameN) HIPCHK(g, fillNegZero(s->frameN, np, s->stream));
           if (s->frameP) HIPCHK(g, fillNegZero(s->frameP, np, s->stream));
         }
@@ -972,7 +1006,7 @@ int groupReduce(sail_ctx* g) {
       sail_ctx* s = g->subs[i];
       if (hipSetDevice(s->device) != hipSuccess) { e = -1; break; }
       e = g_rccl.reduce(s->accum, i == 0 ? r->frame : s->accum, np * 4, kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
-      const bool own = tiles || i == owner;  // the send buffer of this device's AOV maps
+      const bool own = plan[i].send_own_aovs != 0;  // the send buffer of this device's AOV maps
       if (e == 0 && s->aovN)
         e = g_rccl.reduce(own ? s->aovN : s->frameN, i == 0 ? r->frameN : (own ? s->aovN : s->frameN), np * 4,
                           kNcclFloat32, kNcclSum, 0, g->groupComms[i], s->stream);
@@ -991,22 +1025,21 @@ int groupReduce(sail_ctx* g) {
 }
 
 // Host copy of a whole-frame accumulator keeping only what partition (rank, world, mode) holds: its own tiles, or
-// (sample partition) everything on rank 0 and nothing elsewhere (sail_load_accum part -1)
-void ownedPart(const sail_ctx* c, const float* sums, std::vector<float>& out) {
-  const size_t np = (size_t)c->W * c->H;
-  out.assign(np * 4, 0.0f);
-  if (c->world <= 1) { memcpy(out.data(), sums, np * 4 * sizeof(float)); return; }
-  if (c->partMode == SAIL_PART_SAMPLES) {
-    if (c->rank == 0) memcpy(out.data(), sums, np * 4 * sizeof(float));
+// (sample partition) everything on rank 0 and nothing elsewhere (sail_load_accum part -1, sail_plan_keep)
+void keepPart(int W, int H, int rank, int world, int mode, const float* sums, float* out) {
+  const size_t np = (size_t)W * H;
+  if (world <= 1 || (mode == SAIL_PART_SAMPLES && rank == 0)) {
+    if (out != sums) memmove(out, sums, np * 4 * sizeof(float));
     return;
   }
-  const int tx = (c->W + 63) / 64;
-  for (int y = 0; y < c->H; y++)
-    for (int x = 0; x < c->W; x++)
-      if (((y >> 6) * tx + (x >> 6)) % c->world == c->rank) {
-        const size_t i = ((size_t)y * c->W + x) * 4;
-        memcpy(&out[i], &sums[i], 4 * sizeof(float));
-      }
+  if (mode == SAIL_PART_SAMPLES) { memset(out, 0, np * 4 * sizeof(float)); return; }
+  const int tx = (W + 63) / 64;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      const size_t i = ((size_t)y * W + x) * 4;
+      if (((y >> 6) * tx + (x >> 6)) % world != rank) memset(out + i, 0, 4 * sizeof(float));
+      else if (out != sums) memcpy(out + i, sums + i, 4 * sizeof(float));
+    }
 }
 
 }  // namespace
@@ -1147,6 +1180,7 @@ void sail_destroy(sail_ctx* c) {
     return;
   }
   if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->jitHave) sail_jit_hold(c->device, c->jitSpec, -1);  // its queued build, if any, is no longer needed
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm && g_rccl.commDestroy) g_rccl.commDestroy(c->comm);
   for (auto& pr : c->pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1722,10 +1756,9 @@ int sail_reduce(sail_ctx* c, int root) {
   if (int rc = flushQueued(c)) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   const bool isRoot = c->commRank == root;
-  const bool tiles = c->partMode == SAIL_PART_TILES;
   const bool aov = c->aovN || c->aovP;
   // a sample split shows the AOVs of the rank that rendered the last sample: the others send -0 maps
-  const bool own = tiles || c->rank == aovOwner(c->k, c->world);
+  const bool own = planReduce(c->W, c->H, c->rank, c->world, c->partMode, c->k, root).send_own_aovs != 0;
   if (isRoot || (aov && !own)) { if (int rc = ensureFrame(c)) return rc; }
   const size_t np = (size_t)c->W * c->H, count = np * 4;
   if (aov && !own) {
@@ -1772,13 +1805,11 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
   if (!c->subs.empty()) {
     const int nd = (int)c->subs.size();
     if (part < -1 || part >= nd) return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d of %d", part, nd);
-    const uint64_t all = nd >= 64 ? ~0ull : (1ull << nd) - 1ull;
-    if (part >= 0) {  // one part of a checkpoint: the others must follow with the same k before the frame is used
-      if (!c->loadMissing) { c->loadMissing = all; c->loadK = k; }
-      else if (k != c->loadK)
-        return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d has k %llu, the checkpoint being loaded %llu", part,
-                    (unsigned long long)k, (unsigned long long)c->loadK);
-    }
+    // one part of a checkpoint: the others must follow with the same k before the frame is used (sail_plan_load_part)
+    uint64_t missing = c->loadMissing, loadK = c->loadK;
+    if (planLoadPart(&missing, &loadK, nd, part, k) != SAIL_OK)
+      return fail(c, SAIL_E_INVALID, "sail_load_accum: part %d has k %llu, the checkpoint being loaded %llu", part,
+                  (unsigned long long)k, (unsigned long long)c->loadK);
     for (int i = 0; i < nd; i++) {  // part -1: each device keeps its share of the frame; else one part, every k
       if (part == -1 || part == i) {
         if (int rc = sail_load_accum(c->subs[i], part == -1 ? -1 : 0, sums, k)) return relay(c, rc, c->subs[i]);
@@ -1786,7 +1817,8 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
         c->subs[i]->k = k;
       }
     }
-    c->loadMissing = part == -1 ? 0 : (c->loadMissing & ~(1ull << part));
+    c->loadMissing = missing;
+    c->loadK = loadK;
     c->dirty = true;
     return SAIL_OK;
   }
@@ -1797,15 +1829,16 @@ int sail_load_accum(sail_ctx* c, int part, const float* sums, uint64_t k) {
   if (int rc = resetAccum(c)) return rc;  // queued samples, stats and AOVs restart; the accumulator is replaced
   std::vector<float> mine;
   const float* src = sums;
-  if (part == -1 && c->world > 1) { ownedPart(c, sums, mine); src = mine.data(); }
+  if (part == -1 && c->world > 1) {
+    mine.resize((size_t)c->W * c->H * 4);
+    keepPart(c->W, c->H, c->rank, c->world, c->partMode, sums, mine.data());
+    src = mine.data();
+  }
   HIPCHK(c, hipMemcpyAsync(c->accum, src, (size_t)c->W * c->H * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->k = k;
   // this rank's samples among 0 .. k-1 (every one, or those k' = rank mod world of a sample split)
-  if (c->partMode == SAIL_PART_SAMPLES && c->world > 1)
-    c->samplesThisRank = k > (uint64_t)c->rank ? (k - 1 - (uint64_t)c->rank) / (uint64_t)c->world + 1 : 0;
-  else
-    c->samplesThisRank = k;
+  c->samplesThisRank = planReduce(c->W, c->H, c->rank, c->world, c->partMode, k, 0).samples;
   return SAIL_OK;
 }
 
@@ -1895,6 +1928,30 @@ int sail_partition_tiles(int width, int height, int rank, int world, int* out, i
     count++;
   }
   return count;
+}
+
+int sail_plan_reduce(int width, int height, int rank, int world, int mode, uint64_t k, int root, sail_reduce_plan* out) {
+  if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || root < 0 || root >= world || !out ||
+      (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
+    return fail(nullptr, SAIL_E_INVALID, "sail_plan_reduce: bad arguments");
+  *out = planReduce(width, height, rank, world, mode, k, root);
+  return SAIL_OK;
+}
+
+int sail_plan_keep(int width, int height, int rank, int world, int mode, const float* sums, float* out) {
+  if (width <= 0 || height <= 0 || world < 1 || rank < 0 || rank >= world || !sums || !out ||
+      (mode != SAIL_PART_TILES && mode != SAIL_PART_SAMPLES))
+    return fail(nullptr, SAIL_E_INVALID, "sail_plan_keep: bad arguments");
+  keepPart(width, height, rank, world, mode, sums, out);
+  return SAIL_OK;
+}
+
+int sail_plan_load_part(uint64_t* missing, uint64_t* k, int parts, int part, uint64_t k_part) {
+  if (!missing || !k) return fail(nullptr, SAIL_E_INVALID, "sail_plan_load_part: bad arguments");
+  if (int rc = planLoadPart(missing, k, parts, part, k_part))
+    return fail(nullptr, rc, "sail_plan_load_part: part %d of %d (index %llu, checkpoint %llu)", part, parts,
+                (unsigned long long)k_part, (unsigned long long)*k);
+  return SAIL_OK;
 }
 
 int sail_math_probe(int fn, const float* x, const float* y, float* out, int count) {

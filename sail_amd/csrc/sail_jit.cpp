@@ -127,16 +127,7 @@ struct Rtc {
   int major = 0, minor = 0;
 };
 
-// Background builds in flight: a process that exits while one runs inside the compiler would run the compiler's static
-// destructors under it, so exit waits for them (registered after the compiler library is loaded: atexit handlers run in
-// reverse order, so this one runs before that library's destructors).
-std::mutex g_flightMutex;
-std::condition_variable g_flightCv;
-int g_inFlight = 0;
-void waitInFlight() {
-  std::unique_lock<std::mutex> lk(g_flightMutex);
-  g_flightCv.wait(lk, [] { return g_inFlight == 0; });
-}
+void waitInFlight();  // atexit: waits for the build that is running, drops the queued ones (below)
 
 const Rtc* rtc(std::string& err) {
   static Rtc r;
@@ -263,10 +254,11 @@ bool sameCompiler(const std::vector<char>& code, std::string& err) {
   return false;
 }
 
-// one hipRTC compile at a time (the compiler's thread safety is not relied on)
-std::mutex g_compileMutex;
+// one hipRTC compile at a time (the compiler's thread safety is not relied on). On the heap: a fork child replaces it
+// (forkChild), since the parent's build worker may hold it at the fork and does not exist in the child.
+std::mutex* g_compileMutex = new std::mutex;
 int compile(const Rtc& R, const std::string& arch, const Key& k, std::vector<char>& code, std::string& err) {
-  std::lock_guard<std::mutex> lk(g_compileMutex);
+  std::lock_guard<std::mutex> lk(*g_compileMutex);
   const std::string defs = defsFor(k.s);
   hiprtcProgram prog;
   hiprtcResult r = R.create(&prog, defs.c_str(), "sail_jit.hip", sail_jit_src_count, sail_jit_src_texts, sail_jit_src_names);
@@ -315,9 +307,13 @@ struct Entry {
   uint64_t id = 0;
   double compileMs = 0.0;
   int fromCache = 0;
+  bool pinned = false;  // a host-only request waits for it: built even when no context holds the spec (g_mapMutex)
 };
 std::mutex g_mapMutex;
 std::map<std::pair<std::string, Key>, std::shared_ptr<Entry>> g_code;
+// Contexts' claims on specs (sail_jit_hold), under g_mapMutex: the build worker skips a queued build of a context's spec
+// that no context holds any more (refreshJit replaced it), so a scene's current kernel does not wait behind stale builds.
+std::map<std::pair<std::string, Key>, int> g_holds;
 
 // The build identity of a code object: FNV-1a 64 over the sections that hold what runs -- the instructions (.text), the
 // kernel descriptors (.rodata), the code-object metadata (.note: registers, LDS, launch bounds) and any initialised
@@ -374,7 +370,7 @@ int cacheLookup(uint64_t key, std::vector<char>& code) {
   return 0;
 }
 // the background build: hipRTC, then the user cache (and extraDir: sail_jit_code_to_dir)
-void buildEntry(std::shared_ptr<Entry> e, std::string arch, Key k, std::string extraDir) {
+void buildEntry(const std::shared_ptr<Entry>& e, const std::string& arch, const Key& k, const std::string& extraDir) {
   std::vector<char> code;
   std::string err;
   double ms = 0.0;
@@ -391,18 +387,21 @@ void buildEntry(std::shared_ptr<Entry> e, std::string arch, Key k, std::string e
     }
   }
   finish(*e, code, err, ms, 0);
-  {
-    std::lock_guard<std::mutex> lk(g_flightMutex);
-    g_inFlight--;
-  }
-  g_flightCv.notify_all();
 }
 
 struct BuildJob { std::shared_ptr<Entry> e; std::string arch; Key k; std::string extraDir; };
-void* runBuildJob(void* p) {
-  std::unique_ptr<BuildJob> job(static_cast<BuildJob*>(p));
-  buildEntry(job->e, job->arch, job->k, job->extraDir);
-  return nullptr;
+
+// Whether a queued job is still wanted when the worker reaches it: a host-only request (pinned: sail_jit_code, prebuild)
+// always is; a context's only while some context holds its spec. An unwanted entry leaves the map (a later request for
+// the spec starts afresh) and fails with a message no caller sees: nobody holds it, so nobody waits on it.
+bool stillWanted(const BuildJob& j) {
+  std::lock_guard<std::mutex> lk(g_mapMutex);
+  if (j.e->pinned) return true;
+  const auto h = g_holds.find({j.arch, j.k});
+  if (h != g_holds.end() && h->second > 0) return true;
+  const auto it = g_code.find({j.arch, j.k});
+  if (it != g_code.end() && it->second == j.e) g_code.erase(it);
+  return false;
 }
 
 // One build worker for the process, fed by a queue: every compile runs on that same thread, one at a time. (A thread
@@ -411,42 +410,81 @@ void* runBuildJob(void* p) {
 // the synchronous round-4 path used it: always from one thread.) Its stack is large and explicit (256 MB of address
 // space, committed as used): the compiler recurses deeply on the big kernels, and under an "unlimited" stack limit
 // glibc would give a new thread only 2 MB.
+// `running` counts the job the worker has taken (0 or 1): at exit (waitInFlight) the process waits for that compile
+// alone -- exiting inside the compiler would run its static destructors under it -- and drops the queued ones.
 // The queue outlives static destruction (never freed): the worker still waits on its condition variable while the
-// process exits, and destroying a condition variable that has a waiter blocks.
+// process exits, and destroying a condition variable that has a waiter blocks. A fork child gets a fresh queue
+// (forkChild): the parent's worker thread does not exist there.
 struct BuildQueue {
   std::mutex m;
-  std::condition_variable cv;
+  std::condition_variable cv, idle;
   std::vector<BuildJob*> jobs;
   bool workerUp = false;
+  bool exiting = false;
+  int running = 0;
 };
-BuildQueue& queue() {
-  static BuildQueue* q = new BuildQueue;
-  return *q;
+BuildQueue* g_queue = new BuildQueue;
+void dropJob(BuildJob* j, const char* why) {
+  std::vector<char> none;
+  finish(*j->e, none, why, 0.0, 0);
+  delete j;
 }
-void* buildWorker(void*) {
-  BuildQueue& q = queue();
+void* buildWorker(void* arg) {
+  BuildQueue& q = *static_cast<BuildQueue*>(arg);
   for (;;) {
     BuildJob* j;
     {
       std::unique_lock<std::mutex> lk(q.m);
-      q.cv.wait(lk, [&] { return !q.jobs.empty(); });
+      q.cv.wait(lk, [&] { return !q.jobs.empty() || q.exiting; });
+      if (q.exiting) { q.idle.notify_all(); return nullptr; }
       j = q.jobs.front();
       q.jobs.erase(q.jobs.begin());
+      q.running++;
     }
-    runBuildJob(j);
+    if (stillWanted(*j)) {
+      buildEntry(j->e, j->arch, j->k, j->extraDir);
+      delete j;
+    } else {
+      dropJob(j, "build dropped: no context holds this kernel any more");
+    }
+    {
+      std::lock_guard<std::mutex> lk(q.m);
+      q.running--;
+    }
+    q.idle.notify_all();
   }
-  return nullptr;
+}
+// fork: the child has no build worker, and the parent's may hold the queue, map or compile locks at the fork. The prepare
+// handler takes the queue and map locks (the fork happens between jobs' bookkeeping, not inside it); the child gets a
+// fresh queue and compile lock, and forgets the entries still being built in the parent (their jobs ran there), so a
+// request in the child builds them afresh. (A compile the parent's worker was running inside hipRTC at the fork may
+// leave the compiler's own state inconsistent in the child; its next compile then fails and the precompiled kernels
+// serve.)
+void forkPrepare() { g_queue->m.lock(); g_mapMutex.lock(); }
+void forkParent() { g_mapMutex.unlock(); g_queue->m.unlock(); }
+void forkChild() {
+  g_queue = new BuildQueue;  // the parent's (locked, with its jobs) is abandoned
+  g_compileMutex = new std::mutex;
+  for (auto it = g_code.begin(); it != g_code.end();) {
+    std::lock_guard<std::mutex> lk(it->second->m);
+    if (it->second->state == 0) it = g_code.erase(it);
+    else ++it;
+  }
+  g_mapMutex.unlock();
 }
 bool enqueue(BuildJob* job) {
-  BuildQueue& q = queue();
+  static std::once_flag atforkOnce;
+  std::call_once(atforkOnce, [] { pthread_atfork(forkPrepare, forkParent, forkChild); });
+  BuildQueue& q = *g_queue;
   std::lock_guard<std::mutex> lk(q.m);
+  if (q.exiting) return false;
   if (!q.workerUp) {
     pthread_attr_t attr;
     pthread_t tid;
     if (pthread_attr_init(&attr) != 0) return false;
     const bool ok = pthread_attr_setstacksize(&attr, (size_t)256 << 20) == 0 &&
                     pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED) == 0 &&
-                    pthread_create(&tid, &attr, buildWorker, nullptr) == 0;
+                    pthread_create(&tid, &attr, buildWorker, &q) == 0;
     pthread_attr_destroy(&attr);
     if (!ok) return false;
     q.workerUp = true;
@@ -457,32 +495,51 @@ bool enqueue(BuildJob* job) {
 }
 
 // The entry of (arch, spec). At the first request a code object in a disk cache is read here, on the caller's thread
-// (a file read: the warm path of Renderer.update stays in milliseconds); otherwise its build starts in the background.
-std::shared_ptr<Entry> request(const std::string& arch, const Key& k, const std::string& extraDir = std::string()) {
+// (a file read: the warm path of Renderer.update stays in milliseconds), outside the map lock -- other contexts' launches
+// look their kernels up under it; a concurrent request for the same spec finds the entry pending and waits on it --
+// otherwise its build is queued for the background worker. pinned: a host-only caller that waits for the build.
+std::shared_ptr<Entry> request(const std::string& arch, const Key& k, bool pinned, const std::string& extraDir = std::string()) {
   std::shared_ptr<Entry> e;
   {
     std::lock_guard<std::mutex> lk(g_mapMutex);
     auto& slot = g_code[{arch, k}];
-    if (slot) return slot;  // built, being built, or failed (a failed spec is not retried in this process)
-    slot = std::make_shared<Entry>();
-    e = slot;
-    std::vector<char> code;
-    const uint64_t key = cacheKey(arch, k);
-    if (getenv("SAIL_JIT_DEFS"))  // tooling (tools/isa.sh): the source prefix of this spec, to rebuild it with hipcc
-      fprintf(stderr, "sail_jit %s %s\n%s", arch.c_str(), hex16(key).c_str(), defsFor(k.s).c_str());
-    if (const int from = cacheLookup(key, code)) {
-      if (!extraDir.empty()) cacheWrite(extraDir, key, code);
-      finish(*e, code, "", 0.0, from);
-      return e;
+    if (slot) {  // built, being built, or failed (a failed spec is not retried in this process)
+      if (pinned) slot->pinned = true;
+      return slot;
     }
+    slot = std::make_shared<Entry>();
+    slot->pinned = pinned;
+    e = slot;
   }
-  {
-    std::lock_guard<std::mutex> lk(g_flightMutex);
-    g_inFlight++;
+  std::vector<char> code;
+  const uint64_t key = cacheKey(arch, k);
+  if (getenv("SAIL_JIT_DEFS"))  // tooling (tools/isa.sh): the source prefix of this spec, to rebuild it with hipcc
+    fprintf(stderr, "sail_jit %s %s\n%s", arch.c_str(), hex16(key).c_str(), defsFor(k.s).c_str());
+  if (const int from = cacheLookup(key, code)) {
+    if (!extraDir.empty()) cacheWrite(extraDir, key, code);
+    finish(*e, code, "", 0.0, from);
+    return e;
   }
   auto* job = new BuildJob{e, arch, k, extraDir};
-  if (!enqueue(job)) runBuildJob(job);  // no worker thread: build here
+  if (!enqueue(job)) {  // no worker thread (or the process is exiting): build here
+    buildEntry(job->e, job->arch, job->k, job->extraDir);
+    delete job;
+  }
   return e;
+}
+// atexit (registered once the compiler library is loaded: handlers run in reverse order, so this one runs before that
+// library's destructors): wait for the compile the worker is running, drop the queued ones (their entries fail)
+void waitInFlight() {
+  BuildQueue& q = *g_queue;
+  std::vector<BuildJob*> dropped;
+  {
+    std::unique_lock<std::mutex> lk(q.m);
+    q.exiting = true;
+    dropped.swap(q.jobs);
+    q.cv.notify_all();
+    q.idle.wait(lk, [&] { return q.running == 0; });
+  }
+  for (BuildJob* j : dropped) dropJob(j, "build dropped: the process is exiting");
 }
 // wait_ms < 0: until the build is done
 int await(Entry& e, int wait_ms) {
@@ -525,7 +582,7 @@ int sail_jit_kernels(int device, const SailJitSpec& spec, int wait_ms, SailJitKe
   }
   std::string arch;
   if (deviceArch(device, arch, err)) return -1;
-  std::shared_ptr<Entry> e = request(arch, k);
+  std::shared_ptr<Entry> e = request(arch, k, false);
   const int st = await(*e, wait_ms);
   if (st == 0) return 1;
   if (st == 2) { *err = e->err; return -1; }
@@ -556,7 +613,7 @@ int sail_jit_kernels(int device, const SailJitSpec& spec, int wait_ms, SailJitKe
 // buffer (*bytes on entry) is large enough.
 int sail_jit_code(const char* arch, const SailJitSpec& spec, void* code, size_t* bytes, std::string* err) {
   if (!validSpec(spec, err)) return -1;
-  std::shared_ptr<Entry> e = request(arch, Key{spec});
+  std::shared_ptr<Entry> e = request(arch, Key{spec}, true);
   if (await(*e, -1) != 1) { *err = e->err; return -1; }
   const size_t have = *bytes;
   *bytes = e->code.size();
@@ -569,7 +626,7 @@ int sail_jit_code(const char* arch, const SailJitSpec& spec, void* code, size_t*
 
 int sail_jit_code_to_dir(const char* arch, const SailJitSpec& spec, const char* dir, std::string* err) {
   if (!validSpec(spec, err)) return -1;
-  std::shared_ptr<Entry> e = request(arch, Key{spec}, dir && *dir ? std::string(dir) : std::string());
+  std::shared_ptr<Entry> e = request(arch, Key{spec}, true, dir && *dir ? std::string(dir) : std::string());
   if (await(*e, -1) != 1) { *err = e->err; return -1; }
   if (dir && *dir) {  // an entry made earlier in this process wrote only the user cache: write this directory too
     std::vector<char> have;
@@ -577,6 +634,16 @@ int sail_jit_code_to_dir(const char* arch, const SailJitSpec& spec, const char* 
     if (!cacheRead(dir, key, have)) cacheWrite(dir, key, e->code);
   }
   return 0;
+}
+
+void sail_jit_hold(int device, const SailJitSpec& spec, int delta) {
+  std::string arch, err;
+  if (deviceArch(device, arch, &err)) return;
+  std::lock_guard<std::mutex> lk(g_mapMutex);
+  const auto key = std::make_pair(arch, Key{spec});
+  int& h = g_holds[key];
+  h += delta;
+  if (h <= 0) g_holds.erase(key);
 }
 
 void sail_jit_set_cache_dir(const char* dir) {

@@ -32,6 +32,10 @@ struct SailJitKernel {
 // 1 while the code object is still being built and wait_ms allows no more waiting (wait_ms < 0: wait until it is done);
 // -1 with a message when it cannot be built or loaded (the caller then runs the precompiled kernel, same results).
 int sail_jit_kernels(int device, const SailJitSpec& spec, int wait_ms, SailJitKernel* out, std::string* err);
+// A context's claim on the kernel of `spec` on `device` (delta +1 when it adopts the spec, -1 when it drops it): a queued
+// build of a spec no context holds any more is skipped by the build worker, so the scene's current kernel never waits
+// behind builds of specs that a newer scene, partition or switch replaced.
+void sail_jit_hold(int device, const SailJitSpec& spec, int delta);
 // host only: the code object for `arch`, built by the same path (sail_jit_compile, sail_jit_prebuild); blocks
 int sail_jit_code(const char* arch, const SailJitSpec& spec, void* code, size_t* bytes, std::string* err);
 // the on-disk code-object cache directory: nullptr = the default ($XDG_CACHE_HOME or $HOME/.cache, /sail_amd/jit),

@@ -252,3 +252,29 @@ def test_two_precull_compiles_in_one_process(tmp_path):
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
     assert r.stdout.split() == ["0", "0"]
+
+
+def test_fork_child_builds_and_exits(tmp_path):
+    """after fork() the child has no build worker. The child gets a fresh queue, so a compile there runs
+    instead of queueing for a thread that does not exist, and the child's exit does not wait for the parent's jobs.
+    The parent starts its worker with one compile first. No caches."""
+    env = dict(os.environ, AMD_COMGR_CACHE="0")
+    child = (
+        "import ctypes, os, sys\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})\n"
+        "from sail_amd import capi\n"
+        "capi.set_jit_cache('')\n"
+        "lib = capi.load(); n = ctypes.c_size_t(0)\n"
+        "pl = capi.Plugins(0x206, 6, 0, 0)\n"
+        "assert lib.sail_jit_compile(ctypes.byref(pl), 0, None, 0, None, ctypes.byref(n)) == 0\n"
+        "pid = os.fork()\n"
+        "if pid == 0:\n"
+        "    pl2 = capi.Plugins(0x206 | 16, 6, 0, 0)\n"
+        "    rc = lib.sail_jit_compile(ctypes.byref(pl2), 0, None, 0, None, ctypes.byref(n))\n"
+        "    print('child', rc, flush=True)\n"
+        "    os._exit(0 if rc == 0 else 3)\n"
+        "_, st = os.waitpid(pid, 0)\n"
+        "print('parent', os.waitstatus_to_exitcode(st), flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.split() == ["child", "0", "parent", "0"]
