@@ -52,7 +52,7 @@ def load_scene(name="C1"):
         return json.load(f)[name]
 
 
-def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1, spp=8, full=False):
+def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1, spp=8, full=False, frame_hash=False):
     """BASELINE.json's CPU baseline: the single-threaded JS/Node software shader (oracle/sail_soft.js, bit-exact
     with the C++ oracle and the HIP kernel) timed on the host on a bounded sample of the same frame: 32x32
     crops spiralling out from the centre, 8 spp each, until ~budget_s of render time (node start excluded).
@@ -75,19 +75,25 @@ def cpu_baseline_js(sc, masks, mvp, W, H, B, budget_s=12.0, threads=1, spp=8, fu
     job = {"objects": sc["objects"], "n": sc["n"], "texparams": sc["texparams"], "tn": sc["tn"], "lights": sc["lights"],
            "ln": sc["ln"], "masks": list(masks), "W": W, "H": H, "inv": [float(v) for v in inv.reshape(-1)],
            "seeds": [float(v) for v in seeds], "eye": sc["eye"], "spp": spp, "maxBounces": B, "accumMode": 0,
-           "crops": crops, "budgetSeconds": budget_s, "threads": threads}
+           "crops": crops, "budgetSeconds": budget_s, "threads": threads, "writeAccum": bool(frame_hash)}
     with tempfile.TemporaryDirectory() as td:
         jp = os.path.join(td, "job.json")
         with open(jp, "w") as f:
             json.dump(job, f)
         out = subprocess.run([node, os.path.join(ROOT, "oracle", "sail_soft.js"), jp, os.path.join(td, "o")],
                              capture_output=True, text=True, timeout=(600 if full else budget_s * 10 + 60), check=True).stdout
+        sha = None
+        if frame_hash:
+            import hashlib
+            with open(os.path.join(td, "o.accum.f32"), "rb") as f:
+                sha = hashlib.sha256(f.read()).hexdigest()
     r = json.loads(out.strip().splitlines()[-1])
     return {"value": r["segments"] / r["seconds"] / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "implementation": f"oracle/sail_soft.js on Node {r['node']}, "
                               + ("single thread" if threads == 1 else f"{threads} worker_threads"),
             "sample": (f"the whole {W}x{H} frame" if full else f"{r['crops']} centre-out {c}x{c} crops of the frame")
-                      + f", {spp} spp x {B} bounces = {r['segments']} segments (exact count) in {r['seconds']:.2f} s"}
+                      + f", {spp} spp x {B} bounces = {r['segments']} segments (exact count) in {r['seconds']:.2f} s",
+            **({"frame_sha256": sha} if sha else {})}
 
 
 def cpu_baseline_c1_full():
@@ -96,9 +102,13 @@ def cpu_baseline_c1_full():
     sc = load_scene("C1")
     W = H = 256
     mvp = capi.camera(sc["eye"], sc["center"], [0, 1, 0], 55.0, W / H, 1.0, 100.0)
-    r = cpu_baseline_js(sc, capi.plugin_masks(sc["plugins"]), mvp, W, H, 4, spp=64, full=True)
+    r = cpu_baseline_js(sc, capi.plugin_masks(sc["plugins"]), mvp, W, H, 4, spp=64, full=True, frame_hash=True)
     if r:
         r["config"] = "C1: README Cornell box, 256x256, 4 bounces, 64 spp (BASELINE.json configs[0]), in full"
+        # the frame it rendered against the committed hash of the same frame (tests/golden/c1_full_256.json), which
+        # the GPU suite checks the HIP path against (tests/test_c1_full.py)
+        with open(os.path.join(ROOT, "tests", "golden", "c1_full_256.json")) as f:
+            r["frame_matches_fixture"] = r.get("frame_sha256") == json.load(f)["sha256_accum_f32le"]
     return r
 
 

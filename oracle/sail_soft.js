@@ -1150,14 +1150,15 @@ function timedCrops(job, w = 0, nw = 1) {
     sec = Number(process.hrtime.bigint() - t0) / 1e9;
     if (sec >= job.budgetSeconds) break;
   }
-  return { segments, seconds: sec, crops: done };
+  return { segments, seconds: sec, crops: done, accum };
 }
 
 let wt = null;
 try { wt = require('worker_threads'); } catch (e) { wt = null; }
 if (wt && !wt.isMainThread && wt.workerData && wt.workerData.sailCrops) {
   const d = wt.workerData;
-  wt.parentPort.postMessage(timedCrops(d.job, d.w, d.nw));
+  const { segments, seconds, crops } = timedCrops(d.job, d.w, d.nw);  // the counts only, not the frame
+  wt.parentPort.postMessage({ segments, seconds, crops });
 } else if (require.main === module) {
   const fs = require('fs');
   const [jobPath, outPrefix] = process.argv.slice(2);
@@ -1186,6 +1187,8 @@ if (wt && !wt.isMainThread && wt.workerData && wt.workerData.sailCrops) {
     process.stdout.write(JSON.stringify({ n: out.length }) + '\n');
   } else if (job.crops) {
     const r = timedCrops(job);
+    // writeAccum: the frame the timed crops rendered (bench.py's full C1 render checks it against tests/golden)
+    if (job.writeAccum) fs.writeFileSync(outPrefix + '.accum.f32', Buffer.from(r.accum.buffer));
     process.stdout.write(JSON.stringify({ segments: r.segments, seconds: r.seconds, crops: r.crops, node: process.version }) + '\n');
   } else {
     if (job.accumB64) job.accum = new Float32Array(Buffer.from(job.accumB64, 'base64').buffer.slice(0));
