@@ -2,7 +2,11 @@
 """Summarise tools/pmc_mix.sh's two rocprofv3 passes (VALU instruction classes) for the trace kernel into one JSON:
 the counters per dispatch (mean), the kernel they came from, and each class per segment-lane (64 x counter /
 nominal segments of the launch) beside the algorithmic op count, so the executed/algorithmic inflation is attributed.
-Usage: tools/pmc_mix_summary.py gpurun_out/pmc_mix out.json launch_pixels launch_spp bounces workload [ops_per_segment]"""
+Usage: tools/pmc_mix_summary.py gpurun_out/pmc_mix out.json launch_pixels launch_spp bounces workload [ops_per_segment
+       [pmc_summary.json]]
+Refuses (exit 2, no output file) a mix whose passes profiled different builds or no identifiable build, and, when the
+PMC summary the mix will be quoted beside is given (tools/pmc_summary.py's output for the same workload), a mix whose
+kernel_id or launch shape differs from that summary's: a VALU mix is only ever quoted for the build it counted."""
 import collections
 import csv
 import json
@@ -30,6 +34,7 @@ def main():
     pdir, out = sys.argv[1], sys.argv[2]
     px, spp, bounces, workload = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
     ops = float(sys.argv[7]) if len(sys.argv) > 7 else None
+    pair = sys.argv[8] if len(sys.argv) > 8 else None
     c, kernels, durs = {}, set(), {}
     for p in ("mix1", "mix2"):
         vals, ks, d = load(os.path.join(pdir, p, "run_counter_collection.csv"))
@@ -47,12 +52,27 @@ def main():
                 ids |= {json.loads(x)["roofline"].get("kernel_id") for x in f if x.startswith("{") and '"roofline"' in x}
         except OSError:
             ids.add(None)
+    kernel_id = ids.pop() if len(ids) == 1 else None
+    if kernel_id is None:
+        sys.exit("pmc_mix_summary: the passes did not profile one identifiable build (kernel_id missing or differing)")
+    if pair:
+        with open(pair) as f:
+            summ = json.load(f)
+        L = summ.get("launch", {})
+        if summ.get("kernel_id") != kernel_id or summ.get("workload") != workload or \
+                (L.get("pixels"), L.get("spp"), L.get("bounces")) != (px, spp, bounces):
+            print(f"pmc_mix_summary: refused: the mix counted {kernel_id} ({workload}, {px} px x {spp} spp x {bounces}), "
+                  f"{pair} is {summ.get('kernel_id')} ({summ.get('workload')}, {L.get('pixels')} px x {L.get('spp')} spp x "
+                  f"{L.get('bounces')})", file=sys.stderr)
+            sys.exit(2)
     rec = {"kernel": sorted(kernels)[0] if len(kernels) == 1 else sorted(kernels),
-           "kernel_id": ids.pop() if len(ids) == 1 else None, "workload": workload,
+           "kernel_id": kernel_id, "workload": workload,
            "launch": {"pixels": px, "spp": spp, "bounces": bounces, "nominal_segments": segs},
            "source": "tools/pmc_mix.sh (rocprofv3 --pmc, two passes, kernel-trace only), mean per dispatch",
            "dispatch_mean_ns": durs, "counters": c,
            "valu_per_segment_lane": {"total": total, "by_class": per}}
+    if pair:
+        rec["paired_summary"] = os.path.basename(pair)
     if ops:
         rec["valu_per_segment_lane"]["algorithmic_ops_per_segment"] = ops
         rec["valu_per_segment_lane"]["inflation"] = total / ops

@@ -9,7 +9,8 @@
 #   prof_c2|c3|c4|c5 rocprofv3 --kernel-trace --stats of the config's bench (C4 at 64 spp: one launch)
 #   pmc_c2|c3|c4|c5  the four PMC passes of tools/pmc.sh over one launch of the bench's shape, summarised into
 #                    gpurun_out/summ/$TAG_pmc_summary_<cfg>.json
-#   mix_c2|c3        the VALU instruction-mix passes of tools/pmc_mix.sh, summarised the same way
+#   mix_c2|c3|c4     the VALU instruction-mix passes of tools/pmc_mix.sh, summarised the same way and paired with
+#                    the pmc_<cfg> summary of the same session (refused unless both counted the same build)
 #   scale            the per-rank emulation of N = 1/2/4/8 (tools/scaling_probe.py) for C2..C5
 #   variants         tools/variant_bench.py over sail_amd/lib/variants/*.so (VARIANT_ARGS: scene W H B spp ...)
 #   phases           tools/phase_profile.py with the phase-timing build (sail_amd/lib/libsail_hip_phase.so)
@@ -62,10 +63,12 @@ for step in "$@"; do
       c=${step#pmc_}; cfg=$(echo $c | tr a-z A-Z)
       PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=${LS[$c]} bash tools/pmc.sh > /dev/null || exit 7  # one launch
       python tools/pmc_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_summary_$c.json ${PX[$c]} ${LS[$c]} ${BO[$c]} ${WL[$c]} > /dev/null || exit 7 ;;
-    mix_c2|mix_c3)
+    mix_c2|mix_c3|mix_c4)
       c=${step#mix_}; cfg=$(echo $c | tr a-z A-Z)
       PMC_OUT=$OUT/$step PMC_CONFIG=$cfg PMC_SPP=${LS[$c]} bash tools/pmc_mix.sh > /dev/null || exit 8
-      python tools/pmc_mix_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_valu_mix_$c.json ${PX[$c]} ${LS[$c]} ${BO[$c]} ${WL[$c]} ${OPS[$c]} > /dev/null || exit 8 ;;
+      # paired with this session's PMC summary of the same config (run pmc_<cfg> first): refused unless the same build
+      python tools/pmc_mix_summary.py $OUT/$step gpurun_out/summ/${TAG}_pmc_valu_mix_$c.json ${PX[$c]} ${LS[$c]} ${BO[$c]} ${WL[$c]} ${OPS[$c]} \
+        gpurun_out/summ/${TAG}_pmc_summary_$c.json > /dev/null || exit 8 ;;
     scale)
       for a in "C2 1024" "C3 256" "C4 32" "C5 1024"; do
         timeout -k 10 300 python -u tools/scaling_probe.py $a >> $OUT/scale.jsonl 2>&1 || exit 9
