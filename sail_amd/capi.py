@@ -13,7 +13,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsail_hip.so")
+# SAIL_HIP_LIB: another build of the same library (a study variant, tools/study_build.sh), for the profiling tools
+LIB_PATH = os.environ.get("SAIL_HIP_LIB") or os.path.join(_HERE, "lib", "libsail_hip.so")
 
 SAIL_OK = 0
 FLAG_AOV = 1
