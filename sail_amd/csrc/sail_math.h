@@ -126,8 +126,11 @@ SM_D float reduce_spec(float x, int& q) {
 SM_D void sincosf_(float x, float& so, float& co) {
   int q; const float rf = reduce_spec(x, q);
   const float s = sinpoly_f(rf), c = cospoly_f(rf);
-  so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
-  co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
+  // the quadrant by bits, branch-free: odd q swaps sin and cos; the sign flips of -s / -c are sign-bit xors (exact)
+  const bool odd = (q & 1) != 0;
+  const unsigned fs = (unsigned)(q & 2) << 30, fc = (unsigned)((q + 1) & 2) << 30;
+  so = __uint_as_float(__float_as_uint(odd ? c : s) ^ fs);
+  co = __uint_as_float(__float_as_uint(odd ? s : c) ^ fc);
 }
 SM_D float sinf_(float x) { float s, c; sincosf_(x, s, c); return s; }
 SM_D float cosf_(float x) { float s, c; sincosf_(x, s, c); return c; }
