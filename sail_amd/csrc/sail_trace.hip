@@ -132,7 +132,8 @@ D Ray mkRay(V3 o, V3 d) {
   Ray r; r.o = o; r.d = d;
   // one range guard for the three components (rcp_rn guards each)
   const float mx = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)), mn = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
-  if (__builtin_expect(mn >= 0x1p-126f && mx <= 0x1p126f, 1)) {
+  // wave-uniform: the IEEE reciprocals (equal to the Newton step in range) for every lane when some lane is out of range
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(mn >= 0x1p-126f && mx <= 0x1p126f)) == 0ull, 1)) {
     const float y0 = __builtin_amdgcn_rcpf(d.x), y1 = __builtin_amdgcn_rcpf(d.y), y2 = __builtin_amdgcn_rcpf(d.z);
     r.rx = fma_(fma_(-d.x, y0, 1.0f), y0, y0);
     r.ry = fma_(fma_(-d.y, y1, 1.0f), y1, y1);
