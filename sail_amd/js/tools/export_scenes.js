@@ -1,7 +1,8 @@
 'use strict';
 // Serialises the frozen scenes through this build's Sail API (no device needed) to JSON:
 // rows exactly as Renderer.update hands them to libsail_hip.so, the plugin lists, P*MV, eye and the
-// display-filter configuration. Used by bench.py (sail_amd/scenes/frozen.json) and tests/test_js_host.py.
+// display-filter configuration. Used by bench.py (sail_amd/scenes/frozen.json) and tests/test_js_host.py;
+// exportScene is shared with tests/golden/make_fuzz_scenes.js.
 // Usage: node sail_amd/js/tools/export_scenes.js [out.json]
 const fs = require('fs');
 const { SCENES } = require('../scenes');
@@ -26,8 +27,11 @@ function exportScene(scene) {
   return out;
 }
 
-const result = {};
-for (const [name, make] of Object.entries(SCENES)) result[name] = exportScene(make());
-const text = JSON.stringify(result);
-if (process.argv[2]) fs.writeFileSync(process.argv[2], text);
-else process.stdout.write(text);
+if (require.main === module) {
+  const result = {};
+  for (const [name, make] of Object.entries(SCENES)) result[name] = exportScene(make());
+  const text = JSON.stringify(result);
+  if (process.argv[2]) fs.writeFileSync(process.argv[2], text);
+  else process.stdout.write(text);
+}
+module.exports = { exportScene };
