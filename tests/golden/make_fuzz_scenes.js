@@ -115,10 +115,69 @@ function makeScene(seed) {
   return scene;
 }
 
+// Edge scenes: a random scene as above, then the whole scene scaled by 10^-3 .. 10^3 (rows, lights and camera), with
+// degenerate and extreme members added -- zero / negative radii and heights, inverted boxes, zero-area rectangles,
+// disks with the hole wider than the disk, Metal of roughness 0, Glass of eta 1 and below 1, Matte of kd > 1 and
+// sigma 90, checkerboards finer than a pixel, Mix amounts outside [0, 1], negative and huge emission, spot cones of 0
+// and 180 degrees, an area light on a zero-radius sphere -- and the camera far away or inside an object.
+function makeEdgeScene(seed) {
+  const u = xorshift32(0x85EBCA6B ^ (seed * 2246822519));
+  for (let i = 0; i < 8; i++) u();
+  const range = (lo, hi) => lo + (hi - lo) * u();
+  const k = [1e-3, 1e-2, 1, 1e2, 1e3][Math.floor(u() * 5)];
+  const S = (v) => v.map((x) => x * k);
+  const p = () => S([range(0.6, 4.9), range(0.3, 4.8), range(0.2, 5.0)]);
+  const mats = [() => new Sail.Matte(range(1, 3)), () => new Sail.Matte(0.7, 90), () => new Sail.Metal(0),
+    () => new Sail.Glass(1, 1, 1.0), () => new Sail.Glass(1, 1, range(0.5, 0.95)), () => new Sail.Mirror(1),
+    () => new Sail.Metal(0.01, 0.5, 0.001)];
+  const texs = [() => new Sail.Checkerboard(1e-4 * k, 0.5 * k), () => new Sail.Mix([1, 0, 0], [0, 1, 0], range(-2, 3)),
+    () => new Sail.Scale([-1, 0.5, 2], [1, -1, 0.5]), () => Sail.Color.createTexture([range(0, 2), 0, range(0, 2)]),
+    () => new Sail.UV(), () => new Sail.Checkerboard2([1, 1, 1], [0, 0, 0], 1e-4 * k)];
+  const mat = () => mats[Math.floor(u() * mats.length)]();
+  const tex = () => texs[Math.floor(u() * texs.length)]();
+  const scene = new Sail.Scene();
+  const room = Math.floor(u() * 3);
+  if (room === 0) scene.add(new Sail.Cube(S([0, 0, -7]), S([5.56, 5.488, 5.592]), new Sail.Matte(0.7), tex()));
+  else if (room === 1) { const cb = new Sail.Cornellbox([0, 0, -7], [5.56, 5.488, 5.592]); cb.scale(k); scene.add(cb); }
+  const makers = [
+    () => new Sail.Sphere(p(), 0, mat(), tex()),
+    () => new Sail.Sphere(p(), -0.5 * k, mat(), tex()),
+    () => { const a = p(); return new Sail.Cube(a, [a[0] - 0.5 * k, a[1] + 0.5 * k, a[2] - 0.5 * k], mat(), tex()); },
+    () => { const a = p(); return new Sail.Rectangle(a, [a[0], a[1] + 0.5 * k, a[2]], mat(), tex()); },
+    () => new Sail.Disk(p(), 0.5 * k, 0.8 * k, mat(), tex()),
+    () => new Sail.Cone(p(), 0, 0.5 * k, mat(), tex()),
+    () => new Sail.Cone(p(), -0.8 * k, 0.5 * k, mat(), tex()),
+    () => new Sail.Cylinder(p(), 0.8 * k, 0, mat(), tex()),
+    () => new Sail.Paraboloid(p(), 0.8 * k, 0.1 * k, 0.5 * k, mat(), tex()),
+    () => new Sail.Sphere(p(), range(0.3, 0.9) * k, mat(), tex(), [range(-3, -0.5), 2, 2]),
+    () => new Sail.Sphere(p(), range(0.3, 0.9) * k, mat(), tex(), [1e30, 1e30, 1e30]),
+    () => new Sail.Cylinder(p(), range(0.3, 1.5) * k, range(0.2, 0.8) * k, mat(), tex()),
+    () => new Sail.Hyperboloid(p(), [0.5 * k, 0, 0], [0.25 * k, 0.25 * k, k], mat(), tex()),
+  ];
+  const nObj = 3 + Math.floor(u() * 10);
+  for (let i = 0; i < nObj; i++) scene.add(makers[Math.floor(u() * makers.length)]());
+  const lights = [
+    () => new Sail.SpotLight(S([2.78, 5, 2.5]), 0, 0, [5, 5, 5]),
+    () => new Sail.SpotLight(S([2.78, 5, 2.5]), 180, 200, [5, 5, 5]),
+    () => new Sail.PointLight(S([range(0.5, 5), range(0.5, 5), range(0.5, 5)]), [3 * k * k, 3 * k * k, 3 * k * k]),
+    () => new Sail.AreaLight(new Sail.Sphere(S([2.5, 5, 2.5]), 0, new Sail.Matte(0.7), Sail.Color.WHITE), [4, 4, 4]),
+    () => new Sail.AreaLight(new Sail.Disk(S([2.5, 5.3, 2.5]), 0.6 * k, 0.2 * k, new Sail.Matte(0.7), Sail.Color.BLACK), [4, 4, 4]),
+  ];
+  const nLights = Math.floor(u() * 3);
+  for (let i = 0; i < nLights; i++) scene.add(lights[Math.floor(u() * lights.length)]());
+  const view = Math.floor(u() * 3);  // 0: inside the scene, 1: far away, 2: inside the first object's bounds
+  const eye = view === 0 ? S([range(1.5, 4), range(1.5, 4), range(-5, -1)])
+    : view === 1 ? S([range(-3, 9) * 1e3, range(-1, 8) * 1e3, -1e4]) : scene.objects[room === 2 ? 0 : 1].boundbox().min.elements.slice();
+  scene.add(new Sail.Camera(eye, S([range(2, 3.5), range(1.5, 3.5), range(2, 3.5)])));
+  return scene;
+}
+const EDGE_COUNT = 16;
+
 if (require.main === module) {
   const out = {};
   for (let k = 0; k < COUNT; k++) out[`F${String(k).padStart(2, '0')}`] = exportScene(makeScene(k + 1));
+  for (let k = 0; k < EDGE_COUNT; k++) out[`E${String(k).padStart(2, '0')}`] = exportScene(makeEdgeScene(k + 1));
   const file = process.argv[2] || path.join(__dirname, 'fuzz_scenes.json');
   fs.writeFileSync(file, JSON.stringify(out));
 }
-module.exports = { makeScene, COUNT };
+module.exports = { makeScene, makeEdgeScene, COUNT, EDGE_COUNT };
