@@ -278,3 +278,59 @@ def test_fork_child_builds_and_exits(tmp_path):
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
     assert r.stdout.split() == ["child", "0", "parent", "0"]
+
+
+@pytest.mark.gpu
+def test_context_churn_skips_stale_builds_and_exits_promptly(tmp_path):
+    """ADVICE r05 on the box: contexts that set a scene, render without waiting for its run-time kernel and close leave
+    queued builds nobody holds. The worker drops them, so the next context's own kernel waits for at most the build
+    that is running plus its own, not for every stale one; and a process exiting with a build queued waits for the
+    running compile only. Its frame equals the precompiled kernel's bit for bit. No caches (AMD_COMGR_CACHE=0, no
+    user cache): every build is a real hipRTC compile."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = (
+        "import json, sys, time\n"
+        "import numpy as np\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from sail_amd import capi\n"
+        "capi.set_jit_cache('')\n"
+        f"scenes = json.load(open({os.path.join(root, 'tests', 'golden', 'fuzz_scenes.json')!r}))\n"
+        "W, H, B, spp = 24, 16, 4, 2\n"
+        "FLAT = {capi.DEBUG_CULL_MIN_PRIMS: 1000}\n"
+        "def frame(name, debug):\n"
+        "    sc = scenes[name]\n"
+        "    inv, seeds = capi.schedule(np.array(sc['mvp_rowmajor']), W, H, 0, spp)\n"
+        "    ctx = capi.Context(W, H, debug={**FLAT, **debug})\n"
+        "    try:\n"
+        "        ctx.set_scene_dict(sc)\n"
+        "        t0 = time.time()\n"
+        "        ready = ctx.kernel_ready(-1) if debug.get(capi.DEBUG_JIT_WAIT) == -1 else None\n"
+        "        waited = time.time() - t0\n"
+        "        ctx.render_schedule(inv, seeds, sc['eye'], B)\n"
+        "        return ctx.read_accum(), ctx.kernel_name(), waited, ready\n"
+        "    finally:\n"
+        "        ctx.close()\n"
+        "_, k1, t1, r1 = frame('F02', {capi.DEBUG_JIT_WAIT: -1})\n"
+        "for name in ('F03', 'F04', 'F05', 'F06', 'F07', 'F08'):\n"
+        "    frame(name, {capi.DEBUG_JIT_WAIT: 0})\n"
+        "got, k2, t2, r2 = frame('F09', {capi.DEBUG_JIT_WAIT: -1})\n"
+        "want, k3, _, _ = frame('F09', {capi.DEBUG_JIT: 0})\n"
+        "same = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))\n"
+        "frame('F10', {capi.DEBUG_JIT_WAIT: 0})\n"
+        "print(json.dumps({'k1': k1, 'k2': k2, 'k3': k3, 't1': t1, 't2': t2, 'ready': [r1, r2], 'same': same,\n"
+        "                  'end': time.time()}), flush=True)\n")
+    env = dict(os.environ, AMD_COMGR_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=600)
+    done = __import__("time").time()
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    import json
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(dict(res, exit_s=done - res["end"])))
+    assert res["ready"] == [True, True], res
+    assert res["k1"].startswith("sail_trace_kernel_jit") and res["k2"].startswith("sail_trace_kernel_jit"), res
+    assert not res["k3"].startswith("sail_trace_kernel_jit"), res
+    assert res["same"], res
+    t1 = max(res["t1"], 0.5)
+    # six stale builds queued ahead: run one by one they would take about 7 t1; dropped, at most the running one + its own
+    assert res["t2"] < 4 * t1, res
+    assert done - res["end"] < 2 * t1 + 10, (done - res["end"], res)  # exit waits for the running compile only
