@@ -213,3 +213,37 @@ def test_fuzz_pick_equals_oracle(gpu, name):
     widx, wt = oracle.pick(sc, capi.plugin_masks(sc["plugins"])[0], rays)
     assert np.array_equal(idx, widx)
     assert np.array_equal(t.view(np.uint32), wt.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["tiles", "samples"])
+@pytest.mark.parametrize("name", NAMES[2::6])
+def test_fuzz_multi_device_partitions(gpu, name, mode):
+    """the multi-device context over three "devices" on one GPU (sail_create_multi; the frame summed by a kernel) on a
+    130 x 70 frame (three 64 x 64 tiles across, ragged), in 2 + 2 samples with a reduce in between: tiles bit for bit,
+    a sample split to the rounding of its summation order; the AOV maps of the last sample bit for bit in both"""
+    sc = SCENES[name]
+    w, h, b, k = 130, 70, 6, 2
+    inv, seeds = schedule(sc, w, h, 2 * k)
+    part = capi.PART_TILES if mode == "tiles" else capi.PART_SAMPLES
+    ctx = capi.Context(w, h, devices=[0, 0, 0], flags=capi.FLAG_AOV)
+    try:
+        ctx.set_scene_dict(sc)
+        ctx.set_partition(0, 1, part)
+        ctx.render_schedule(inv[:k], seeds[:k], sc["eye"], b)
+        ctx.read_accum()
+        ctx.render_schedule(inv[k:], seeds[k:], sc["eye"], b)
+        got = ctx.read_accum()
+        _, gn, gp = ctx.readback(aov=True)
+    finally:
+        ctx.close()
+    want, wn, wp, _ = oracle_frame(name, w, h, 2 * k, b)
+    assert bit_equal(gn, wn).all() and bit_equal(gp, wp).all()
+    assert (got[..., 3] == 2 * k).all()
+    if mode == "tiles":
+        same = bit_equal(got, want)
+        assert same.all(), f"{name}: {int((~same).sum())} of {got.size} channels differ"
+    else:
+        fin = np.isfinite(want)
+        assert (np.isfinite(got) == fin).all()
+        assert np.allclose(got[fin], want[fin], rtol=1e-5, atol=1e-5)
