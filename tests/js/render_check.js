@@ -1,5 +1,5 @@
 'use strict';
-// Renders a frozen scene through Sail.Renderer -> N-API -> libsail_hip.so and writes the raw accumulator
+// Renders a frozen (or random) scene through Sail.Renderer -> N-API -> libsail_hip.so and writes the raw accumulator
 // (and the canvas pixels) for tests/test_js_host.py to compare with the CPU oracle. Needs an MI355X.
 // argv: scene W H spp bounces mode(sum|mix) api(samples|frames|progressive|resume) out_prefix [filter [filter-r]]
 // env SAIL_TEST_DEVICES=0,0,0: a multi-device Renderer ({devices: [...]}); progressive = half the samples as
@@ -8,7 +8,9 @@ const fs = require('fs');
 const Sail = require('../../sail_amd/js');
 const { SCENES } = require('../../sail_amd/js/scenes');
 const [name, W, H, spp, B, mode, api, out, filter, filterR] = process.argv.slice(2);
-const scene = SCENES[name]();
+// fuzz:F07 / fuzz:E03: a seeded random / edge scene of tests/golden/make_fuzz_scenes.js, built here by the Sail API
+const fuzz = name.startsWith('fuzz:') ? require('../golden/make_fuzz_scenes') : null;
+const scene = fuzz ? (name[5] === 'E' ? fuzz.makeEdgeScene : fuzz.makeScene)(+name.slice(6) + 1) : SCENES[name]();
 if (filter) {  // the reference's scene.filter = name; scene.filter.addParam('r', ...) flow
   scene.filter = filter;
   if (filterR) scene.filter.addParam('r', filterR);

@@ -247,3 +247,25 @@ def test_fuzz_multi_device_partitions(gpu, name, mode):
         fin = np.isfinite(want)
         assert (np.isfinite(got) == fin).all()
         assert np.allclose(got[fin], want[fin], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(NODE is None, reason="node not installed")
+@pytest.mark.parametrize("name,mode,api,devices", [("F05", "sum", "frames", None), ("F19", "mix", "samples", None),
+                                                   ("F23", "sum", "progressive", "0,0,0"), ("E05", "sum", "resume", None),
+                                                   ("E13", "mix", "frames", "0,0")])
+def test_fuzz_through_the_js_renderer(tmp_path, name, mode, api, devices):
+    """the whole drop-in stack on random scenes: the scene built by the Sail JS API in Node (tests/js/render_check.js),
+    Renderer.update / render through N-API into libsail_hip.so, against the oracle over the fixture's rows"""
+    w, h, spp, b = 40, 30, 4, 6
+    prefix = str(tmp_path / name)
+    env = dict(os.environ, **({"SAIL_TEST_DEVICES": devices} if devices else {}))
+    subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "render_check.js"), "fuzz:" + name, str(w), str(h), str(spp),
+                    str(b), mode, api, prefix], cwd=ROOT, check=True, timeout=300, env=env)
+    got = np.fromfile(prefix + ".accum.f32", dtype=np.float32).reshape(h, w, 4)
+    sc = SCENES[name]
+    inv, seeds = schedule(sc, w, h, spp)
+    want = oracle.render(sc, capi.plugin_masks(sc["plugins"]), w, h, inv, seeds, sc["eye"], b,
+                         accum_mode=oracle.ACC_SUM if mode == "sum" else oracle.ACC_MIX)
+    same = bit_equal(got, want)
+    assert same.all(), f"{name}: {int((~same).sum())} of {got.size} channels differ"
